@@ -1,0 +1,181 @@
+/* include/pgtg.h -- C ABI of the MI355X-native batched PGTG environment (libpgtg_hip.so).
+ *
+ * The reference (Inuri04/pgtg) has no FFI: its hot path sits behind the Gymnasium Env API of
+ * `PGTGEnv` (pgtg/environment.py:297-1281, registered as "pgtg-v4" in pgtg/__init__.py:7).  Each
+ * entry point below replaces one piece of that surface for a BATCH of independent environments
+ * resident in HBM; the Python facade in pgtg_amd/ (PGTGEnv, PGTGVecEnv) binds it with ctypes.
+ *
+ *   pgtg_create       <- PGTGEnv.__init__(map_path, **kwargs)          environment.py:302-515
+ *   pgtg_reset        <- PGTGEnv.reset(seed=...)                        environment.py:581-656
+ *   pgtg_step         <- PGTGEnv.step(action) + same-step auto-reset    environment.py:1092-1281
+ *   pgtg_set_outputs  <- the obs/reward/terminated/truncated/info return values (device buffers)
+ *   pgtg_get_cars / pgtg_get_env_state <- get_info() fields             environment.py:1538-1578
+ *   pgtg_set_agent / pgtg_add_car      <- test-style state overrides (env.position = ..., env.cars.append)
+ *   pgtg_get_map_plan <- EpisodeMap.map_plan / save_map                 pgtg/map.py:173-184
+ *   pgtg_get_counters <- (new) device-side env-step / episode counters
+ *
+ * Conventions: all pointers named *_dev are device pointers (hipMalloc'd or torch data_ptr) on the
+ * handle's device; everything else is host memory.  Calls on one handle are serialised by the
+ * caller and enqueued on the handle's HIP stream (pgtg_set_stream); they do not synchronise unless
+ * documented.  Every entry point returns PGTG_OK (0) or a negative PGTG_E_* code; the message is
+ * available from pgtg_last_error(handle).
+ */
+#ifndef PGTG_H_
+#define PGTG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGTG_ABI_VERSION 1
+
+/* status codes (Python facade maps them to the reference's exception types) */
+#define PGTG_OK 0
+#define PGTG_E_INVALID -1      /* invalid configuration / argument  -> ValueError            */
+#define PGTG_E_DONE -2         /* step on a finished env (no auto-reset) -> RuntimeError       */
+#define PGTG_E_DEVICE -3       /* HIP runtime error                  -> RuntimeError           */
+#define PGTG_E_UNSUPPORTED -4  /* outside this build's limits        -> ValueError             */
+#define PGTG_E_MAP -5          /* map without route / no start square / empty route choice      */
+
+/* limits of this build */
+#define PGTG_MAX_TILES 64      /* width*height of the tile map */
+#define PGTG_MAX_CHANNELS 48
+#define PGTG_MAX_RULES 8
+#define PGTG_MAX_WINDOW 15     /* observation window side (9 fixed, 2*s+1 sliding) */
+
+/* observation channel codes (one per key of the reference's obs["map"] dict) */
+enum {
+  PGTG_CH_ZERO = 0,        /* names that never occur on a square: all zeros */
+  PGTG_CH_WALL = 1,        /* "walls" / "wall" */
+  PGTG_CH_GOALS = 2,       /* "goals": subgoal or final goal */
+  PGTG_CH_TRAFFIC = 3,     /* "traffic": a car on the square */
+  PGTG_CH_TL_GREEN = 4,    /* "traffic_light" key -> traffic_light_{green,yellow,red} */
+  PGTG_CH_TL_YELLOW = 5,
+  PGTG_CH_TL_RED = 6,
+  PGTG_CH_START = 7,
+  PGTG_CH_SUBGOAL = 8,
+  PGTG_CH_USED_SUBGOAL = 9,
+  PGTG_CH_FINAL_GOAL = 10,
+  PGTG_CH_ICE = 11,
+  PGTG_CH_BROKEN = 12,
+  PGTG_CH_SAND = 13,
+  PGTG_CH_SPAWNER = 14,
+  PGTG_CH_LANE0 = 32       /* + lane id 0..31, "car_lane <route> <type>" in sorted order */
+};
+
+typedef struct {
+  int32_t tile_exits;       /* rule tile_type "NESW" bits as mask (bit0 north); -1 = never */
+  int32_t speed_sq_min;     /* admissible vx^2+vy^2 interval for velocity_range (fp64 sqrt) */
+  int32_t speed_sq_max;
+  int32_t min_traffic;
+  int32_t min_matching_traffic;
+  /* weight[d][r]: maneuvers with agent direction d listing route r;
+   * d: 0 south_to_north 1 west_to_east 2 north_to_south 3 east_to_west 4 stationary 5 near_goal */
+  uint8_t weight[6][20];
+} PgtgRule;
+
+/* Raw constructor kwargs (pgtg/environment.py:302-359) plus the fixed map of map_path. */
+typedef struct {
+  int32_t abi_version;                 /* = PGTG_ABI_VERSION */
+  int32_t width, height;               /* random_map_width / random_map_height */
+  double pct_connections;              /* random_map_percentage_of_connections */
+  int32_t start_mode, goal_mode;       /* 0 (x,y,dir)  1 (x,y)  2 "random" */
+  int32_t start_x, start_y, start_dir; /* dir: 0 north 1 east 2 south 3 west; x/y may be -1 */
+  int32_t goal_x, goal_y, goal_dir;
+  int32_t min_distance;                /* random_map_minimum_distance_between_start_and_goal, -1 None */
+  double obstacle_probability;
+  double w_ice, w_broken, w_sand, w_tl;
+  int32_t n_channels;
+  int32_t channels[PGTG_MAX_CHANNELS];
+  int32_t sliding, sliding_size, next_subgoal;
+  double sum_subgoals_reward, final_goal_bonus, crash_penalty, tl_violation_penalty;
+  double standing_still_penalty, visited_penalty;
+  double ice_probability, street_damage_probability, sand_probability, traffic_density;
+  int32_t phase_dur[3];
+  int32_t ignore_traffic_collisions;
+  double profile_pct[5];               /* conservative, normal, aggressive, elderly, reckless */
+  int32_t separate_reward_cost;
+  int32_t n_rules;
+  PgtgRule rules[PGTG_MAX_RULES];
+  /* fixed map (map_path): tiles row-major [y*w+x] */
+  int32_t fixed_map, fm_w, fm_h;
+  uint8_t fm_exits[PGTG_MAX_TILES];
+  int8_t fm_obst_type[PGTG_MAX_TILES]; /* -1 none, 0 ice 1 broken road 2 sand 3 traffic_light */
+  int8_t fm_obst_mask[PGTG_MAX_TILES]; /* -1 none, 0..13 (tools/gen_tables.py order) */
+  int32_t fm_start[3], fm_goal[3];
+  /* vector-env options (no reference equivalent; pgtg/train.py:21-41 wraps with TimeLimit) */
+  int32_t autoreset;                   /* 1: same-step auto-reset (gymnasium/SB3 vector semantics) */
+  int32_t max_episode_steps;           /* TimeLimit truncation, 0 = none */
+} PgtgConfig;
+
+/* Output buffers (device pointers, caller-owned, contiguous).  NULL = not produced. */
+typedef struct {
+  uint8_t* obs;            /* [N][n_channels][win][win] uint8 one-hot ([c][x][y] like the reference) */
+  int32_t* position;       /* [N][2] */
+  int32_t* velocity;       /* [N][2] */
+  int32_t* next_subgoal;   /* [N] (use_next_subgoal_direction) */
+  double* reward;          /* [N] */
+  double* cost;            /* [N] (separate_reward_cost) */
+  uint8_t* terminated;     /* [N] */
+  uint8_t* truncated;      /* [N] */
+  uint8_t* final_obs;      /* [N][n_channels][win][win]: terminal observation of envs reset this step */
+  int32_t* final_position; /* [N][2] */
+  int32_t* final_velocity; /* [N][2] */
+  int32_t* final_next_subgoal; /* [N] */
+  uint8_t* braking;        /* [N] info['traffic_rules']['braking_applied'] */
+} PgtgOutputs;
+
+typedef struct {
+  int32_t x, y, vx, vy;
+  int32_t terminated, flat_tire, phase, elapsed;
+  int32_t n_cars, next_car_id, path_len, error;
+  uint32_t spawn_counter;
+  uint64_t seed, used_subgoals;
+} PgtgEnvState;
+
+typedef struct {
+  int32_t id, x, y, route, profile, patience, delay;
+} PgtgCar;
+
+typedef struct pgtg_handle pgtg_handle;
+
+int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_handle** out);
+int pgtg_destroy(pgtg_handle* h);
+/* Queue work on this stream (hipStream_t); NULL = the null stream. */
+int pgtg_set_stream(pgtg_handle* h, void* stream);
+int pgtg_set_outputs(pgtg_handle* h, const PgtgOutputs* out);
+/* Seeded reset of env i with seeds_host[i] (NULL: seed_base + global index), only where
+ * mask_dev[i] != 0 (NULL: all).  Writes the reset observation to the bound outputs. */
+int pgtg_reset(pgtg_handle* h, const uint64_t* seeds_host, uint64_t seed_base, const uint8_t* mask_dev);
+/* Unseeded reset (next spawn block of each env's seed sequence) where mask_dev[i] != 0. */
+int pgtg_reset_unseeded(pgtg_handle* h, const uint8_t* mask_dev);
+/* One tick for every env.  actions_dev: [N] uint8 in [0, 9). */
+int pgtg_step(pgtg_handle* h, const uint8_t* actions_dev);
+/* Fill [N] uint8 actions with a counter-based uniform hash of (seed, env, t) -- synthetic rollouts. */
+int pgtg_random_actions(pgtg_handle* h, uint8_t* actions_dev, uint64_t seed, uint64_t t);
+/* Host-synchronising introspection (copies device state). */
+int pgtg_get_env_state(pgtg_handle* h, uint64_t env, PgtgEnvState* st);
+int pgtg_get_cars(pgtg_handle* h, uint64_t env, PgtgCar* cars, int32_t cap, int32_t* n);
+int pgtg_get_map_plan(pgtg_handle* h, uint64_t env, int32_t* w, int32_t* h_, uint8_t* exits, int8_t* otype,
+                      int8_t* omask, int32_t* start3, int32_t* goal3);
+int pgtg_set_agent(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t vx, int32_t vy);
+int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t route, int32_t profile);
+/* Re-emit the observation of every env into the bound outputs (after set_agent/add_car). */
+int pgtg_observe(pgtg_handle* h);
+/* steps (env-steps executed) and episodes (resets) since create, summed over envs; synchronises. */
+int pgtg_get_counters(pgtg_handle* h, uint64_t* env_steps, uint64_t* episodes);
+/* Number of envs whose last step reported an error (PGTG_E_DONE / PGTG_E_MAP); synchronises. */
+int pgtg_error_count(pgtg_handle* h, uint64_t* n_errors, int32_t* first_code);
+int pgtg_window(const pgtg_handle* h);
+uint64_t pgtg_num_envs(const pgtg_handle* h);
+const char* pgtg_last_error(const pgtg_handle* h);
+/* Kernel timing of the last pgtg_step on the handle's stream (ms, HIP events); -1 if unavailable. */
+float pgtg_last_step_ms(pgtg_handle* h);
+int pgtg_enable_timing(pgtg_handle* h, int32_t on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PGTG_H_ */

@@ -1,0 +1,257 @@
+// pgtg_amd/csrc/pgtg_device.h -- device-side data layout and numpy-exact RNG for the batched
+// PGTG kernels (gfx950).  One lane owns one environment; all per-env state is structure-of-arrays
+// in HBM (coalesced 8/16/32-byte records, see DESIGN.md "Data layout in HBM").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pgtg.h"
+
+namespace pgtg {
+
+constexpr int kTile = 9;
+constexpr int kMaxTiles = PGTG_MAX_TILES;
+constexpr int kMaxEdges = 256;    // directed interior edges of a <=64-tile grid (<= 224)
+constexpr int kMaxBorder = 192;   // border-connection candidates (<= 2w+2h-2)
+constexpr int kMaxWin = PGTG_MAX_WINDOW;
+constexpr int kMaskWords = (kMaxWin * kMaxWin + 31) / 32;  // 8
+constexpr int kBlock = 256;       // lanes (= envs) per workgroup for the step kernels
+
+// agent flags (EnvRec.w2 bits 16..23)
+constexpr uint32_t kFlagTerminated = 1u << 0;
+constexpr uint32_t kFlagFlatTire = 1u << 1;
+constexpr uint32_t kFlagBraking = 1u << 2;
+constexpr uint32_t kFlagTruncated = 1u << 3;
+
+// per-square feature flags (square_flags)
+constexpr uint32_t SQ_WALL = 1u << 0, SQ_SUBGOAL = 1u << 1, SQ_USED = 1u << 2, SQ_FINAL = 1u << 3,
+                   SQ_START = 1u << 4, SQ_ICE = 1u << 5, SQ_BROKEN = 1u << 6, SQ_SAND = 1u << 7,
+                   SQ_TLIGHT = 1u << 8, SQ_SPAWNER = 1u << 9;
+
+// Tile-plan entry (u16): bits 0-3 exits (N,E,S,W), 4-6 obstacle type (0 none, 1 ice, 2 broken
+// road, 3 sand, 4 traffic light), 7-10 obstacle mask id, 11-13 subgoal exit direction + 1.
+__host__ __device__ inline uint32_t plan_exits(uint32_t p) { return p & 15u; }
+__host__ __device__ inline uint32_t plan_otype(uint32_t p) { return (p >> 4) & 7u; }
+__host__ __device__ inline uint32_t plan_omask(uint32_t p) { return (p >> 7) & 15u; }
+__host__ __device__ inline int plan_sgdir(uint32_t p) { return (int)((p >> 11) & 7u) - 1; }
+
+// EnvRec (32 B, one uint4 pair per env):
+//  w0 = px | py<<16 (int16)   w1 = vx | vy<<16 (int16)   w2 = phase | flags<<16 | path_len<<24
+//  w3 = elapsed steps         w4 = start_tile | start_dir<<8 | goal_tile<<16 | goal_dir<<24
+//  w5 = spawn counter (SeedSequence children spawned)   w6,w7 = used-subgoal tile mask (u64)
+struct EnvRec {
+  uint4 a, b;
+};
+
+struct DevCfg {
+  int32_t tw, th, nt, W, H;
+  int32_t fixed_map;
+  uint16_t fixed_plan[kMaxTiles];
+  uint32_t fixed_sg;
+  int32_t start_mode, goal_mode, sx, sy, sdir, gx, gy, gdir, min_distance;
+  int32_t n_edges, keep;
+  uint8_t ea[kMaxEdges], eb[kMaxEdges], ed[kMaxEdges], erev[kMaxEdges];
+  int32_t n_border, n_border_add;
+  uint8_t bt[kMaxBorder], bd[kMaxBorder];
+  double obstacle_probability;
+  double obst_cdf[4];
+  double ice_p, broken_p, sand_p;
+  int32_t phase_total, phase_g, phase_gy;
+  int32_t ignore_collisions, separate_cost, autoreset, max_steps;
+  double crash_penalty, final_goal_bonus, tl_penalty, still_penalty, visited_penalty;
+  double ind_reward[kMaxTiles + 1];
+  int32_t n_channels, win, sliding, ss, next_subgoal, generic_channels;
+  int32_t channels[PGTG_MAX_CHANNELS];
+  int32_t need_car, need_ice, need_broken, need_sand;
+  double density;
+  double profile_cdf[5];
+  int32_t car_cap;
+  int32_t n_rules;
+  PgtgRule rules[PGTG_MAX_RULES];
+  int32_t nsd_off, nsd_pitch;   // nsd table index (dx+off)*pitch + (dy+off)
+  int32_t cmp_off, cmp_pitch;   // compass table index
+  int32_t vis_pitch, vis_words; // visited bitset: ((x+2)*vis_pitch + (y+2))
+  int32_t plan_stride;          // u16 per env in the global tile-plan array (multiple of 8)
+  int32_t obs_bytes;            // n_channels * win * win
+  int32_t mask_words;           // ceil(win*win/32)
+};
+
+// one PCG64 stream, SoA over envs
+struct DevStream {
+  uint64_t* shi;
+  uint64_t* slo;
+  uint64_t* ihi;
+  uint64_t* ilo;
+  uint64_t* buf;  // bit 32 = has_uint32, low 32 = buffered value
+};
+
+struct DevState {
+  uint64_t n;
+  EnvRec* rec;
+  uint64_t* seed;
+  uint16_t* plan;         // [n][plan_stride]
+  DevStream car, ice, broken, sand;
+  uint32_t* visited;      // [n][vis_words] or null
+  uint32_t* cars;         // [n][car_cap][2] packed cars or null (traffic)
+  uint32_t* car_ids;      // [n][car_cap]
+  uint32_t* car_meta;     // [n]: n_cars | next_car_id (2 x u32)
+  uint8_t* err;           // [n] last error code (negated PGTG_E_*)
+  unsigned long long* counters;  // [2]: env steps, episodes
+  const int8_t* nsd_tab;
+  const int8_t* cmp_tab;
+};
+
+// ------------------------------------------------------------------------------------------------
+// numpy-exact RNG (Generator(PCG64(SeedSequence(seed, spawn_key=(k,))))): SeedSequence mixing
+// (numpy/random/bit_generator.pyx), PCG64 XSL-RR 128-bit LCG with next_uint32 high-half buffering,
+// Lemire bounded ints (distributions.c buffered_bounded_lemire_uint32), 53-bit doubles.
+// ------------------------------------------------------------------------------------------------
+struct Pcg {
+  uint64_t shi, slo, ihi, ilo;
+  uint32_t buf, has;
+};
+
+__device__ __forceinline__ void pcg_step(Pcg& g) {
+  const uint64_t MH = 0x2360ED051FC65DA4ull, ML = 0x4385DF649FCCF645ull;
+  uint64_t lo = g.slo * ML;
+  uint64_t hi = __umul64hi(g.slo, ML) + g.slo * MH + g.shi * ML;
+  uint64_t nlo = lo + g.ilo;
+  hi += g.ihi + (nlo < lo ? 1ull : 0ull);
+  g.slo = nlo;
+  g.shi = hi;
+}
+__device__ __forceinline__ uint64_t pcg_next64(Pcg& g) {
+  pcg_step(g);
+  uint64_t x = g.shi ^ g.slo;
+  unsigned rot = (unsigned)(g.shi >> 58);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+__device__ __forceinline__ uint32_t pcg_next32(Pcg& g) {
+  if (g.has) {
+    g.has = 0;
+    return g.buf;
+  }
+  uint64_t v = pcg_next64(g);
+  g.has = 1;
+  g.buf = (uint32_t)(v >> 32);
+  return (uint32_t)v;
+}
+__device__ __forceinline__ double pcg_double(Pcg& g) {
+  return (double)(pcg_next64(g) >> 11) * (1.0 / 9007199254740992.0);
+}
+// integers(0, n) == choice(n): n == 1 draws nothing
+__device__ __forceinline__ uint32_t pcg_int(Pcg& g, uint32_t n) {
+  uint32_t rng = n - 1u;
+  if (rng == 0u) return 0u;
+  uint32_t excl = n;
+  uint64_t m = (uint64_t)pcg_next32(g) * excl;
+  uint32_t left = (uint32_t)m;
+  if (left < excl) {
+    uint32_t thr = (0xffffffffu - rng) % excl;
+    while (left < thr) {
+      m = (uint64_t)pcg_next32(g) * excl;
+      left = (uint32_t)m;
+    }
+  }
+  return (uint32_t)(m >> 32);
+}
+// choice(k, p=p) with the host-normalised CDF (cumsum(p)/cumsum[-1]): searchsorted(u, 'right')
+template <int K>
+__device__ __forceinline__ int pcg_choice_cdf(Pcg& g, const double* cdf) {
+  double u = pcg_double(g);
+  int i = 0;
+#pragma unroll
+  for (int j = 0; j < K - 1; j++) i += (u < cdf[j]) ? 0 : 1;
+  // cdf is non-decreasing: i counts entries <= u, clamp for safety
+  return i < K ? i : K - 1;
+}
+
+__device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t& hc) {
+  v ^= hc;
+  hc *= 0x931e8875u;
+  v *= hc;
+  v ^= v >> 16;
+  return v;
+}
+__device__ __forceinline__ uint32_t ss_mix(uint32_t x, uint32_t y) {
+  uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y;
+  r ^= r >> 16;
+  return r;
+}
+// SeedSequence pool after mixing the (zero-padded) run entropy of `seed`; hc continues from it.
+struct SeedPool {
+  uint32_t p[4];
+  uint32_t hc;
+};
+__device__ __forceinline__ SeedPool ss_pool(uint64_t seed) {
+  SeedPool s;
+  uint32_t hc = 0x43b0d7e5u;
+  uint32_t e[4] = {(uint32_t)seed, (uint32_t)(seed >> 32), 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < 4; i++) s.p[i] = ss_hashmix(e[i], hc);
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+      if (a != b) s.p[b] = ss_mix(s.p[b], ss_hashmix(s.p[a], hc));
+  s.hc = hc;
+  return s;
+}
+// child stream with spawn key (key,): mix the key word, generate_state(4, uint64), seed PCG64
+__device__ __forceinline__ Pcg ss_child(const SeedPool& sp, uint32_t key) {
+  uint32_t p[4] = {sp.p[0], sp.p[1], sp.p[2], sp.p[3]};
+  uint32_t hc = sp.hc;
+#pragma unroll
+  for (int d = 0; d < 4; d++) p[d] = ss_mix(p[d], ss_hashmix(key, hc));
+  uint32_t w[8];
+  uint32_t hb = 0x8b51f9ddu;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t v = p[i & 3];
+    v ^= hb;
+    hb *= 0x58f38dedu;
+    v *= hb;
+    v ^= v >> 16;
+    w[i] = v;
+  }
+  uint64_t v0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32), v1 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  uint64_t v2 = (uint64_t)w[4] | ((uint64_t)w[5] << 32), v3 = (uint64_t)w[6] | ((uint64_t)w[7] << 32);
+  Pcg g;
+  // inc = (initseq << 1) | 1 with initseq = v2:v3
+  g.ihi = (v2 << 1) | (v3 >> 63);
+  g.ilo = (v3 << 1) | 1ull;
+  g.shi = 0;
+  g.slo = 0;
+  g.has = 0;
+  g.buf = 0;
+  pcg_step(g);
+  uint64_t lo = g.slo + v1;
+  g.shi = g.shi + v0 + (lo < g.slo ? 1ull : 0ull);
+  g.slo = lo;
+  pcg_step(g);
+  return g;
+}
+
+__device__ __forceinline__ Pcg stream_load(const DevStream& s, uint64_t i) {
+  Pcg g;
+  g.shi = s.shi[i];
+  g.slo = s.slo[i];
+  g.ihi = s.ihi[i];
+  g.ilo = s.ilo[i];
+  uint64_t b = s.buf[i];
+  g.buf = (uint32_t)b;
+  g.has = (uint32_t)(b >> 32) & 1u;
+  return g;
+}
+__device__ __forceinline__ void stream_store_state(const DevStream& s, uint64_t i, const Pcg& g) {
+  s.shi[i] = g.shi;
+  s.slo[i] = g.slo;
+  s.buf[i] = (uint64_t)g.buf | ((uint64_t)g.has << 32);
+}
+__device__ __forceinline__ void stream_store_all(const DevStream& s, uint64_t i, const Pcg& g) {
+  stream_store_state(s, i, g);
+  s.ihi[i] = g.ihi;
+  s.ilo[i] = g.ilo;
+}
+
+}  // namespace pgtg

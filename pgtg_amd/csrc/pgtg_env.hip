@@ -1,0 +1,1498 @@
+// pgtg_amd/csrc/pgtg_env.hip -- MI355X (gfx950) kernels of the batched PGTG environment.
+//
+// One lane advances one independent environment (wave64, 256 lanes per workgroup).  Each lane
+// reproduces, bit for bit, the reference's per-env control flow:
+//   step   : pgtg/environment.py:1092-1281 (phase, cars, acceleration, braking, decomposition,
+//            sub-step crash/goal/subgoal/red-light/ice/broken-road/sand handling, penalties)
+//   reset  : pgtg/environment.py:581-656 with pgtg/map_generator.py:43-472 (procedural map) and
+//            pgtg/parser.py:13-166 + pgtg/map.py:11-42 (map compilation) done in-kernel
+//   obs    : pgtg/environment.py:1344-1536
+// The map is never materialised per square: each env keeps a 2-byte-per-tile plan (staged in LDS
+// for the kernel's lifetime) and square features are recomputed from constant 81-bit tile tables.
+// Observations are staged as per-channel bitmasks in LDS and written to HBM cooperatively by the
+// whole workgroup with 16-byte coalesced stores.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <array>
+#include <string>
+#include <vector>
+
+#include "pgtg_device.h"
+
+namespace pgtg {
+namespace dv {
+#define PGTG_TBL_QUAL __constant__ static const
+#include "pgtg_tables.h"
+#undef PGTG_TBL_QUAL
+}  // namespace dv
+namespace hs {
+#define PGTG_TBL_QUAL static const
+#include "pgtg_tables.h"
+#undef PGTG_TBL_QUAL
+}  // namespace hs
+
+// ------------------------------------------------------------------------------------------------
+// small device helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bit81(const uint32_t* m3, int sq) { return (m3[sq >> 5] >> (sq & 31)) & 1u; }
+
+// exit segment a local square belongs to (north (3..5,0), east (8,3..5), south (3..5,8), west (0,3..5))
+__device__ __forceinline__ int seg_dir(int lx, int ly) {
+  bool mx = (unsigned)(lx - 3) <= 2u, my = (unsigned)(ly - 3) <= 2u;
+  if (ly == 0 && mx) return 0;
+  if (lx == 8 && my) return 1;
+  if (ly == 8 && mx) return 2;
+  if (lx == 0 && my) return 3;
+  return -1;
+}
+
+struct EnvView {
+  int px, py, vx, vy;
+  uint32_t phase, flags, path_len, elapsed;
+  uint32_t sg, spawn;
+  uint64_t used;
+};
+
+__device__ __forceinline__ EnvView rec_load(const EnvRec* r, uint64_t i) {
+  EnvRec e = r[i];
+  EnvView v;
+  v.px = (int)(int16_t)(e.a.x & 0xffffu);
+  v.py = (int)(int16_t)(e.a.x >> 16);
+  v.vx = (int)(int16_t)(e.a.y & 0xffffu);
+  v.vy = (int)(int16_t)(e.a.y >> 16);
+  v.phase = e.a.z & 0xffffu;
+  v.flags = (e.a.z >> 16) & 0xffu;
+  v.path_len = e.a.z >> 24;
+  v.elapsed = e.a.w;
+  v.sg = e.b.x;
+  v.spawn = e.b.y;
+  v.used = (uint64_t)e.b.z | ((uint64_t)e.b.w << 32);
+  return v;
+}
+__device__ __forceinline__ void rec_store(EnvRec* r, uint64_t i, const EnvView& v) {
+  EnvRec e;
+  e.a.x = ((uint32_t)v.px & 0xffffu) | ((uint32_t)v.py << 16);
+  e.a.y = ((uint32_t)v.vx & 0xffffu) | ((uint32_t)v.vy << 16);
+  e.a.z = (v.phase & 0xffffu) | ((v.flags & 0xffu) << 16) | (v.path_len << 24);
+  e.a.w = v.elapsed;
+  e.b.x = v.sg;
+  e.b.y = v.spawn;
+  e.b.z = (uint32_t)v.used;
+  e.b.w = (uint32_t)(v.used >> 32);
+  r[i] = e;
+}
+
+// Per-lane LDS view of the env's tile plan.  Lane stride is an odd number of dwords so that 64
+// lanes reading the same tile index hit distinct banks.
+struct Plan {
+  uint16_t* p;
+  __device__ __forceinline__ uint32_t operator[](int t) const { return p[t]; }
+};
+
+// features of square (x, y) inside the map (pgtg/parser.py:47-155 semantics, see file header)
+__device__ __forceinline__ uint32_t square_flags(const DevCfg& c, const Plan& pl, const EnvView& v, int x, int y) {
+  int tx = x / kTile, ty = y / kTile;
+  int lx = x - tx * kTile, ly = y - ty * kTile;
+  int t = ty * c.tw + tx;
+  uint32_t p = pl[t];
+  uint32_t ex = plan_exits(p);
+  int sq = lx * 9 + ly;
+  uint32_t f = 0;
+  uint32_t wall = bit81(dv::kTileWall[ex], sq);
+  if (wall) f |= SQ_WALL;
+  int d = seg_dir(lx, ly);
+  if (d >= 0 && ((ex >> d) & 1u)) {
+    if (plan_sgdir(p) == d) f |= ((v.used >> t) & 1ull) ? SQ_USED : SQ_SUBGOAL;
+    if ((int)(v.sg & 0xffu) == t && (int)((v.sg >> 8) & 0xffu) == d) f |= SQ_START;
+    if ((int)((v.sg >> 16) & 0xffu) == t && (int)(v.sg >> 24) == d) f |= SQ_FINAL;
+  }
+  uint32_t ot = plan_otype(p);
+  if (ot && !wall && bit81(dv::kObstMask[plan_omask(p)], sq)) f |= SQ_ICE << (ot - 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t square_lanes(const DevCfg& c, const Plan& pl, int x, int y) {
+  int tx = x / kTile, ty = y / kTile;
+  int lx = x - tx * kTile, ly = y - ty * kTile;
+  uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
+  return ex ? dv::kLanes[ex][lx * 9 + ly] : 0u;
+}
+__device__ __forceinline__ bool square_spawner(const DevCfg& c, const Plan& pl, int x, int y) {
+  int tx = x / kTile, ty = y / kTile;
+  int lx = x - tx * kTile, ly = y - ty * kTile;
+  uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
+  if (!ex) return false;
+  int sq = lx * 9 + ly;
+  if (bit81(dv::kLaneSpawner[ex], sq)) return true;
+  uint32_t l = dv::kLanes[ex][sq];
+  return (tx == 0 && (l >> 31 & 1u)) || (tx == c.tw - 1 && (l >> 30 & 1u)) || (ty == 0 && (l >> 29 & 1u)) ||
+         (ty == c.th - 1 && (l >> 28 & 1u));
+}
+__device__ __forceinline__ bool inside(const DevCfg& c, int x, int y) {
+  return (unsigned)x < (unsigned)c.W && (unsigned)y < (unsigned)c.H;
+}
+__device__ __forceinline__ int phase_color(const DevCfg& c, uint32_t ph) {
+  return (int)ph < c.phase_g ? 0 : ((int)ph < c.phase_gy ? 1 : 2);
+}
+
+// ------------------------------------------------------------------------------------------------
+// reset: seeding, procedural map, compilation, start square  (pgtg/environment.py:581-656)
+// ------------------------------------------------------------------------------------------------
+__device__ void rand_pos(const DevCfg& c, Pcg& r, int& x, int& y) {  // map_generator.py:602-626
+  switch (pcg_int(r, 4)) {
+    case 0: x = (int)pcg_int(r, c.tw); y = 0; break;
+    case 1: x = c.tw - 1; y = (int)pcg_int(r, c.th); break;
+    case 2: x = (int)pcg_int(r, c.tw); y = c.th - 1; break;
+    default: x = 0; y = (int)pcg_int(r, c.th); break;
+  }
+}
+__device__ int rand_dir(const DevCfg& c, Pcg& r, int x, int y) {  // map_generator.py:574-599
+  int o[4], n = 0;
+  if (y == 0) o[n++] = 0;
+  if (x == c.tw - 1) o[n++] = 1;
+  if (y == c.th - 1) o[n++] = 2;
+  if (x == 0) o[n++] = 3;
+  int k = (int)pcg_int(r, (uint32_t)n);
+  return k == 0 ? o[0] : (k == 1 ? o[1] : (k == 2 ? o[2] : o[3]));
+}
+
+template <int NW>
+__device__ __forceinline__ int select_kth(const uint64_t (&m)[NW], int k) {
+  int base = 0, res = -1;
+#pragma unroll
+  for (int w = 0; w < NW; w++) {
+    int cnt = __popcll(m[w]);
+    if (res < 0) {
+      if (k < cnt) {
+        uint64_t x = m[w];
+        for (int i = 0; i < k; i++) x &= x - 1ull;
+        res = base + __ffsll((long long)x) - 1;
+      } else {
+        k -= cnt;
+      }
+    }
+    base += 64;
+  }
+  return res;
+}
+template <int NW>
+__device__ __forceinline__ void clear_bit(uint64_t (&m)[NW], int i) {
+#pragma unroll
+  for (int w = 0; w < NW; w++)
+    if (w == (i >> 6)) m[w] &= ~(1ull << (i & 63));
+}
+
+// start tile reaches goal tile in the symmetric tile graph given by the four exit masks
+__device__ __forceinline__ bool connected(uint64_t hN, uint64_t hE, uint64_t hS, uint64_t hW, int w, int s, int g) {
+  uint64_t R = 1ull << s, goal = 1ull << g;
+  for (;;) {
+    uint64_t N = R | ((R & hN) >> w) | ((R & hS) << w) | ((R & hE) << 1) | ((R & hW) >> 1);
+    if (N & goal) return true;
+    if (N == R) return false;
+    R = N;
+  }
+}
+
+// generate_map (map_generator.py:43-189) -> tile plan (exits + obstacles) in LDS, start/goal
+__device__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* plan, int& st_t, int& st_d, int& gl_t, int& gl_d) {
+  const int w = c.tw;
+  // chose_random_start_and_goal_position_and_direction (map_generator.py:475-571)
+  int s0, s1, s2 = c.sdir, g0, g1, g2 = c.gdir;
+  int slen, glen;
+  if (c.start_mode == 2) {
+    rand_pos(c, r, s0, s1);
+    slen = 2;
+  } else {
+    s0 = c.sx != -1 ? c.sx : c.tw - 1;
+    s1 = c.sy != -1 ? c.sy : c.th - 1;
+    slen = c.start_mode == 1 ? 2 : 3;
+  }
+  if (c.goal_mode == 2) {
+    rand_pos(c, r, g0, g1);
+    glen = 2;
+  } else {
+    g0 = c.gx != -1 ? c.gx : c.tw - 1;
+    g1 = c.gy != -1 ? c.gy : c.th - 1;
+    glen = c.goal_mode == 1 ? 2 : 3;
+  }
+  int guard = 0;  // the reference loops forever on unsatisfiable settings; the kernel must not
+  if (c.min_distance >= 0) {
+    while (abs(s0 - g0) + abs(s1 - g1) < c.min_distance && ++guard < 100000) {
+      rand_pos(c, r, s0, s1);
+      slen = 2;
+      rand_pos(c, r, g0, g1);
+      glen = 2;
+    }
+  }
+  if (slen == 2) s2 = rand_dir(c, r, s0, s1);
+  if (glen == 2) g2 = rand_dir(c, r, g0, g1);
+  while (s0 == g0 && s1 == g1 && s2 == g2 && ++guard < 100000) {
+    if (c.start_mode == 2) rand_pos(c, r, s0, s1);
+    if (c.start_mode != 0) s2 = rand_dir(c, r, s0, s1);
+    if (c.goal_mode == 2) rand_pos(c, r, g0, g1);
+    if (c.goal_mode != 0) g2 = rand_dir(c, r, g0, g1);
+    if (c.start_mode == 0 && c.goal_mode == 0) break;  // rejected on the host
+  }
+  st_t = s1 * w + s0;
+  st_d = s2;
+  gl_t = g1 * w + g0;
+  gl_d = g2;
+
+  // generate_map_graph (map_generator.py:192-266).  removable_edges keeps graph-theory's nested
+  // dict order (host table ea/eb); an edge pair stays removed iff start->end stays connected,
+  // which is exactly the outcome of the reference's BFS-path test + re-add.
+  uint64_t hN = 0, hE = 0, hS = 0, hW = 0;
+  uint64_t L[4] = {0, 0, 0, 0};
+  for (int e = 0; e < c.n_edges; e++) {
+    int a = c.ea[e];
+    switch (c.ed[e]) {
+      case 0: hN |= 1ull << a; break;
+      case 1: hE |= 1ull << a; break;
+      case 2: hS |= 1ull << a; break;
+      default: hW |= 1ull << a; break;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    int lo = q * 64, n = c.n_edges - lo;
+    L[q] = n >= 64 ? ~0ull : (n <= 0 ? 0ull : ((1ull << n) - 1ull));
+  }
+  int nrem = c.n_edges, count = c.n_edges;
+  while (count > c.keep && nrem > 0) {
+    int k = (int)pcg_int(r, (uint32_t)nrem);
+    int e = select_kth<4>(L, k);
+    int e2 = c.erev[e];
+    clear_bit<4>(L, e);
+    clear_bit<4>(L, e2);
+    nrem -= 2;
+    int a = c.ea[e], b = c.eb[e], d = c.ed[e];
+    uint64_t ma = 1ull << a, mb = 1ull << b;
+    uint64_t sN = hN, sE = hE, sS = hS, sW = hW;
+    switch (d) {  // remove a->b and b->a
+      case 0: hN &= ~ma; hS &= ~mb; break;
+      case 1: hE &= ~ma; hW &= ~mb; break;
+      case 2: hS &= ~ma; hN &= ~mb; break;
+      default: hW &= ~ma; hE &= ~mb; break;
+    }
+    count -= 2;
+    if (!connected(hN, hE, hS, hW, w, st_t, gl_t)) {
+      hN = sN; hE = sE; hS = sS; hW = sW;
+      count += 2;
+    }
+  }
+  // map_graph_to_tile_map_object (map_generator.py:269-334): exits straight into the LDS plan
+  for (int t = 0; t < c.nt; t++)
+    plan[t] = (uint16_t)((uint32_t)((hN >> t) & 1ull) | (uint32_t)((hE >> t) & 1ull) << 1 |
+                         (uint32_t)((hS >> t) & 1ull) << 2 | (uint32_t)((hW >> t) & 1ull) << 3);
+  plan[st_t] |= (uint16_t)(1u << st_d);
+  plan[gl_t] |= (uint16_t)(1u << gl_d);
+  // add_connections_to_borders (map_generator.py:337-371), candidate list from the host
+  uint64_t B[3] = {0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    int n = c.n_border - q * 64;
+    B[q] = n >= 64 ? ~0ull : (n <= 0 ? 0ull : ((1ull << n) - 1ull));
+  }
+  int nb = c.n_border;
+  for (int k = 0; k < c.n_border_add; k++) {
+    int j = select_kth<3>(B, (int)pcg_int(r, (uint32_t)nb));
+    clear_bit<3>(B, j);
+    nb--;
+    plan[c.bt[j]] |= (uint16_t)(1u << c.bd[j]);
+  }
+  // add_obstacles_to_map (map_generator.py:374-472)
+  if (c.obstacle_probability > 0.0) {
+    for (int t = 0; t < c.nt; t++) {
+      uint32_t e = plan[t];
+      double u = pcg_double(r);
+      if (u < c.obstacle_probability && e != 0u) {
+        int ot = pcg_choice_cdf<4>(r, c.obst_cdf);
+        uint32_t om;
+        if (ot != 3) {
+          om = pcg_int(r, 8);
+        } else {
+          int n = __popc(e);
+          uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0, o4 = 0, o5 = 0;
+          int m = 0;
+          auto push = [&](uint32_t val) {
+            if (m == 0) o0 = val; else if (m == 1) o1 = val; else if (m == 2) o2 = val;
+            else if (m == 3) o3 = val; else if (m == 4) o4 = val; else o5 = val;
+            m++;
+          };
+          if (e & 1u) push(8);
+          if (e & 2u) push(9);
+          if (e & 4u) push(10);
+          if (e & 8u) push(11);
+          if ((e & 1u) && (e & 4u) && n >= 3) push(12);
+          if ((e & 2u) && (e & 8u) && n >= 3) push(13);
+          int k = (int)pcg_int(r, (uint32_t)m);
+          om = k == 0 ? o0 : k == 1 ? o1 : k == 2 ? o2 : k == 3 ? o3 : k == 4 ? o4 : o5;
+        }
+        plan[t] = (uint16_t)(e | (uint32_t)(ot + 1) << 4 | om << 7);
+      }
+    }
+  }
+}
+
+// parse_map_object's shortest path (graph-theory Dijkstra == FIFO BFS, neighbours N,E,S,W)
+// -> subgoal directions in the plan; returns the path length (num_subgoals) or 0.
+__device__ int compile_path(const DevCfg& c, uint16_t* plan, uint8_t* q, uint8_t* par, int s, int g) {
+  const int w = c.tw, h = c.th;
+  uint64_t seen = 1ull << s;
+  int qh = 0, qt = 0;
+  q[qt++] = (uint8_t)s;
+  par[s] = 255;
+  bool found = false;
+  while (qh < qt) {
+    int v = q[qh++];
+    if (v == g) {
+      found = true;
+      break;
+    }
+    int x = v % w, y = v / w;
+    uint32_t e = plan_exits(plan[v]);
+    int nb[4] = {v - w, v + 1, v + w, v - 1};
+    bool ok[4] = {(e & 1u) && y > 0, (e & 2u) && x < w - 1, (e & 4u) && y < h - 1, (e & 8u) && x > 0};
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      if (ok[d] && !((seen >> nb[d]) & 1ull)) {
+        seen |= 1ull << nb[d];
+        par[nb[d]] = (uint8_t)v;
+        q[qt++] = (uint8_t)nb[d];
+      }
+    }
+  }
+  if (!found) return 0;
+  int len = 1, ch = g;
+  while (par[ch] != 255) {
+    int p = par[ch];
+    int d = (ch == p - w) ? 0 : (ch == p + 1) ? 1 : (ch == p + w) ? 2 : 3;
+    plan[p] = (uint16_t)((plan[p] & ~(7u << 11)) | (uint32_t)(d + 1) << 11);
+    ch = p;
+    len++;
+  }
+  return len;
+}
+
+// The full per-env reset.  `key` = spawn counter (5 children per episode).  Returns 0 or -code.
+__device__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, uint16_t* plan, uint8_t* q,
+                         uint8_t* par) {
+  uint64_t seed = S.seed[i];
+  SeedPool sp = ss_pool(seed);
+  uint32_t k = v.spawn;
+  Pcg map_rng = ss_child(sp, k + 0u);
+  if (c.need_car) stream_store_all(S.car, i, ss_child(sp, k + 1u));
+  if (c.need_ice) stream_store_all(S.ice, i, ss_child(sp, k + 2u));
+  if (c.need_broken) stream_store_all(S.broken, i, ss_child(sp, k + 3u));
+  if (c.need_sand) stream_store_all(S.sand, i, ss_child(sp, k + 4u));
+  v.spawn = k + 5u;
+  int st_t, st_d, gl_t, gl_d;
+  if (c.fixed_map) {
+    for (int t = 0; t < c.nt; t++) plan[t] = c.fixed_plan[t];
+    st_t = (int)(c.fixed_sg & 0xffu);
+    st_d = (int)((c.fixed_sg >> 8) & 0xffu);
+    gl_t = (int)((c.fixed_sg >> 16) & 0xffu);
+    gl_d = (int)(c.fixed_sg >> 24);
+  } else {
+    generate_map(c, map_rng, plan, st_t, st_d, gl_t, gl_d);
+  }
+  v.sg = (uint32_t)st_t | (uint32_t)st_d << 8 | (uint32_t)gl_t << 16 | (uint32_t)gl_d << 24;
+  int len = compile_path(c, plan, q, par, st_t, gl_t);
+  v.used = 0;
+  v.path_len = (uint32_t)len;
+  v.flags = 0;
+  v.phase = 0;
+  v.elapsed = 0;
+  v.vx = v.vy = 0;
+  if (len == 0 || !((plan_exits(plan[st_t]) >> st_d) & 1u)) {
+    v.px = v.py = 0;
+    return PGTG_E_MAP;
+  }
+  // starters: the start tile's exit segment in the start direction, x-major (pgtg/map.py:31-34)
+  int j = (int)pcg_int(map_rng, 3);
+  int tx = st_t % c.tw, ty = st_t / c.tw, lx, ly;
+  switch (st_d) {
+    case 0: lx = 3 + j; ly = 0; break;
+    case 1: lx = 8; ly = 3 + j; break;
+    case 2: lx = 3 + j; ly = 8; break;
+    default: lx = 0; ly = 3 + j; break;
+  }
+  v.px = tx * kTile + lx;
+  v.py = ty * kTile + ly;
+  if (S.visited) {
+    uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
+    for (int q2 = 0; q2 < c.vis_words; q2++) vis[q2] = 0;
+    int b = (v.px + 2) * c.vis_pitch + (v.py + 2);
+    vis[b >> 5] |= 1u << (b & 31);
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// observation -> per-channel bitmasks in LDS (pgtg/environment.py:1344-1506)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t chan_bit(int code, uint32_t f, uint32_t lanes, bool spawner, int color) {
+  switch (code) {
+    case PGTG_CH_WALL: return f & SQ_WALL ? 1u : 0u;
+    case PGTG_CH_GOALS: return f & (SQ_SUBGOAL | SQ_FINAL) ? 1u : 0u;
+    case PGTG_CH_TL_GREEN: return (color == 0 && (f & SQ_TLIGHT)) ? 1u : 0u;
+    case PGTG_CH_TL_YELLOW: return (color == 1 && (f & SQ_TLIGHT)) ? 1u : 0u;
+    case PGTG_CH_TL_RED: return (color == 2 && (f & SQ_TLIGHT)) ? 1u : 0u;
+    case PGTG_CH_START: return f & SQ_START ? 1u : 0u;
+    case PGTG_CH_SUBGOAL: return f & SQ_SUBGOAL ? 1u : 0u;
+    case PGTG_CH_USED_SUBGOAL: return f & SQ_USED ? 1u : 0u;
+    case PGTG_CH_FINAL_GOAL: return f & SQ_FINAL ? 1u : 0u;
+    case PGTG_CH_ICE: return f & SQ_ICE ? 1u : 0u;
+    case PGTG_CH_BROKEN: return f & SQ_BROKEN ? 1u : 0u;
+    case PGTG_CH_SAND: return f & SQ_SAND ? 1u : 0u;
+    case PGTG_CH_SPAWNER: return spawner ? 1u : 0u;
+    default:
+      if (code >= PGTG_CH_LANE0 && code < PGTG_CH_LANE0 + 32) return (lanes >> (code - PGTG_CH_LANE0)) & 1u;
+      return 0u;
+  }
+}
+
+struct ObsInfo {
+  int x0, y0;          // window origin
+  int posx, posy;      // observation position
+  int nsd;             // next_subgoal_direction
+};
+
+// nearest subgoal / final goal square from (x, y): min Manhattan, x-major first (environment.py:1471-1480)
+__device__ bool nearest_goal_square(const DevCfg& c, const Plan& pl, const EnvView& v, int x, int y, int& bx, int& by) {
+  int best = 0x7fffffff;
+  bool found = false;
+  int gl_t = (int)((v.sg >> 16) & 0xffu), gl_d = (int)(v.sg >> 24);
+  for (int t = 0; t < c.nt; t++) {
+    uint32_t p = pl[t];
+    int d = -1;
+    int sd = plan_sgdir(p);
+    if (sd >= 0 && !((v.used >> t) & 1ull)) d = sd;
+    for (int pass = 0; pass < 2; pass++) {
+      int dd = pass == 0 ? d : (t == gl_t ? gl_d : -1);
+      if (dd < 0) continue;
+      int tx = (t % c.tw) * kTile, ty = (t / c.tw) * kTile;
+      for (int j = 0; j < 3; j++) {
+        int sx, sy;
+        switch (dd) {
+          case 0: sx = tx + 3 + j; sy = ty; break;
+          case 1: sx = tx + 8; sy = ty + 3 + j; break;
+          case 2: sx = tx + 3 + j; sy = ty + 8; break;
+          default: sx = tx; sy = ty + 3 + j; break;
+        }
+        int dist = abs(sx - x) + abs(sy - y);
+        if (!found || dist < best || (dist == best && (sx < bx || (sx == bx && sy < by)))) {
+          found = true;
+          best = dist;
+          bx = sx;
+          by = sy;
+        }
+      }
+    }
+  }
+  return found;
+}
+
+__device__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v, uint32_t* masks,
+                          ObsInfo& oi) {
+  int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
+  int tx = pix / kTile, ty = piy / kTile;
+  int color = phase_color(c, v.phase);
+  const int MW = c.mask_words;
+  if (!c.sliding) {
+    oi.x0 = tx * kTile;
+    oi.y0 = ty * kTile;
+    oi.posx = pix - oi.x0;
+    oi.posy = piy - oi.y0;
+  } else {
+    oi.x0 = v.px - c.ss;
+    oi.y0 = v.py - c.ss;
+    oi.posx = oi.posy = c.ss;
+  }
+  if (!c.sliding && !c.generic_channels) {
+    // fast path: the window is exactly one tile -> 81-bit table algebra
+    int t = ty * c.tw + tx;
+    uint32_t p = pl[t];
+    uint32_t ex = plan_exits(p);
+    uint32_t W3[3], SG[3] = {0, 0, 0}, US[3] = {0, 0, 0}, FI[3] = {0, 0, 0}, ST[3] = {0, 0, 0}, OB[3] = {0, 0, 0};
+    int sd = plan_sgdir(p);
+    bool used = (v.used >> t) & 1ull;
+    int st_t = (int)(v.sg & 0xffu), st_d = (int)((v.sg >> 8) & 0xffu);
+    int gl_t = (int)((v.sg >> 16) & 0xffu), gl_d = (int)(v.sg >> 24);
+    uint32_t ot = plan_otype(p);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      W3[k] = dv::kTileWall[ex][k];
+      if (sd >= 0 && ((ex >> sd) & 1u)) (used ? US : SG)[k] = dv::kExitSeg[sd][k];
+      if (t == gl_t && ((ex >> gl_d) & 1u)) FI[k] = dv::kExitSeg[gl_d][k];
+      if (t == st_t && ((ex >> st_d) & 1u)) ST[k] = dv::kExitSeg[st_d][k];
+      if (ot) OB[k] = dv::kObstMask[plan_omask(p)][k] & ~W3[k];
+    }
+    for (int ci = 0; ci < c.n_channels; ci++) {
+      int code = c.channels[ci];
+      uint32_t* m = masks + ci * MW;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        uint32_t val;
+        switch (code) {
+          case PGTG_CH_WALL: val = W3[k]; break;
+          case PGTG_CH_GOALS: val = SG[k] | FI[k]; break;
+          case PGTG_CH_TL_GREEN: val = (color == 0 && ot == 4) ? OB[k] : 0u; break;
+          case PGTG_CH_TL_YELLOW: val = (color == 1 && ot == 4) ? OB[k] : 0u; break;
+          case PGTG_CH_TL_RED: val = (color == 2 && ot == 4) ? OB[k] : 0u; break;
+          case PGTG_CH_START: val = ST[k]; break;
+          case PGTG_CH_SUBGOAL: val = SG[k]; break;
+          case PGTG_CH_USED_SUBGOAL: val = US[k]; break;
+          case PGTG_CH_FINAL_GOAL: val = FI[k]; break;
+          case PGTG_CH_ICE: val = ot == 1 ? OB[k] : 0u; break;
+          case PGTG_CH_BROKEN: val = ot == 2 ? OB[k] : 0u; break;
+          case PGTG_CH_SAND: val = ot == 3 ? OB[k] : 0u; break;
+          default: val = 0u; break;  // PGTG_CH_ZERO, PGTG_CH_TRAFFIC (filled by the traffic pass)
+        }
+        m[k] = val;
+      }
+    }
+  } else {
+    const int win = c.win;
+    for (int ci = 0; ci < c.n_channels; ci++)
+      for (int k = 0; k < MW; k++) masks[ci * MW + k] = 0u;
+    for (int i = 0; i < win; i++)
+      for (int j = 0; j < win; j++) {
+        int x = oi.x0 + i, y = oi.y0 + j;
+        uint32_t f, lanes = 0;
+        bool sp = false;
+        if (inside(c, x, y)) {
+          f = square_flags(c, pl, v, x, y);
+          if (c.generic_channels) {
+            lanes = square_lanes(c, pl, x, y);
+            sp = square_spawner(c, pl, x, y);
+          }
+        } else {
+          f = c.sliding ? SQ_WALL : 0u;  // get_map_cutout fill {"wall"} for sliding windows
+        }
+        int b = i * win + j;
+        for (int ci = 0; ci < c.n_channels; ci++)
+          masks[ci * MW + (b >> 5)] |= chan_bit(c.channels[ci], f, lanes, sp, color) << (b & 31);
+      }
+  }
+  oi.nsd = -1;
+  if (c.next_subgoal) {
+    int t = ty * c.tw + tx;
+    int sd = plan_sgdir(pl[t]);
+    int gl_t = (int)((v.sg >> 16) & 0xffu);
+    int nsd = sd >= 0 ? sd : (t == gl_t ? (int)(v.sg >> 24) : -1);
+    if (nsd == -1 || c.sliding) {
+      int bx = 0, by = 0;
+      if (nearest_goal_square(c, pl, v, pix, piy, bx, by))
+        nsd = S.nsd_tab[(bx - pix + c.nsd_off) * c.nsd_pitch + (by - piy + c.nsd_off)];
+    }
+    oi.nsd = nsd;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// step (pgtg/environment.py:1092-1281) for one lane; returns 0 or -code
+// ------------------------------------------------------------------------------------------------
+constexpr int ACCX[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
+constexpr int ACCY[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1};
+
+struct StepResult {
+  double reward, cost;
+};
+
+__device__ int env_step(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, const Plan& pl, int action,
+                        StepResult& res) {
+  res.reward = 0.0;
+  res.cost = 0.0;
+  if (v.flags & (kFlagTerminated | kFlagTruncated)) return PGTG_E_DONE;
+  if ((unsigned)action > 8u) return PGTG_E_INVALID;
+  v.phase = (v.phase + 1u) % (uint32_t)c.phase_total;
+  const int ax = ACCX[action], ay = ACCY[action];
+  double reward = 0.0, perf = 0.0, cost = 0.0;
+  int cx = v.px, cy = v.py;
+  v.vx += ax;
+  v.vy += ay;
+  v.flags &= ~kFlagBraking;
+  if (abs(v.vx) > 30000 || abs(v.vy) > 30000) return PGTG_E_UNSUPPORTED;
+  Pcg ice, broken, sand;
+  if (c.need_ice) ice = stream_load(S.ice, i);
+  if (c.need_broken) broken = stream_load(S.broken, i);
+  if (c.need_sand) sand = stream_load(S.sand, i);
+  bool used_ice = false, used_broken = false, used_sand = false;
+  // _decompose_velocity (environment.py:693-748) evaluated lazily: part k is cum(k+1) - cum(k)
+  const int dx = v.vx, dy = v.vy;
+  const int adx = abs(dx), ady = abs(dy);
+  const int n = max(adx, ady);
+  const bool xmajor = adx >= ady;
+  const int smaj = xmajor ? (dx > 0 ? 1 : -1) : (dy > 0 ? 1 : -1);
+  double m = 0.0;
+  if (dx != 0 && dy != 0) m = xmajor ? (double)dy / (double)adx : (double)dx / (double)ady;
+  int prev_minor = 0;
+  const int gl_t = (int)((v.sg >> 16) & 0xffu), gl_d = (int)(v.sg >> 24);
+  const int color = phase_color(c, v.phase);
+  for (int k = 0; k <= n; k++) {
+    // crash: outside, wall (cars: traffic pass)
+    if (!inside(c, cx, cy)) {
+      if (c.separate_cost) cost += c.crash_penalty; else reward -= c.crash_penalty;
+      v.flags |= kFlagTerminated;
+      break;
+    }
+    uint32_t f = square_flags(c, pl, v, cx, cy);
+    if (f & SQ_WALL) {
+      if (c.separate_cost) cost += c.crash_penalty; else reward -= c.crash_penalty;
+      v.flags |= kFlagTerminated;
+      break;
+    }
+    if (f & SQ_FINAL) {
+      double add = c.ind_reward[v.path_len] + c.final_goal_bonus;
+      if (c.separate_cost) perf += add; else reward += add;
+      v.flags |= kFlagTerminated;
+      break;
+    }
+    if (f & SQ_SUBGOAL) {
+      if (c.separate_cost) perf += c.ind_reward[v.path_len]; else reward += c.ind_reward[v.path_len];
+      // set_subgoals_to_used: the flood fill covers exactly this tile's subgoal segment
+      v.used |= 1ull << ((cy / kTile) * c.tw + cx / kTile);
+    }
+    if (k == n) break;
+    // part k
+    int ii = k + 1, pxp, pyp;
+    int minor = 0;
+    if (dx == 0 || dy == 0) {
+      minor = 0;
+    } else {
+      double t = (double)ii * m;
+      t = t + 0.5;
+      minor = (int)floor(t);
+    }
+    if (xmajor) {
+      pxp = smaj;
+      pyp = (dy == 0) ? 0 : minor - prev_minor;
+    } else {
+      pyp = smaj;
+      pxp = (dx == 0) ? 0 : minor - prev_minor;
+    }
+    prev_minor = minor;
+    // red light at the next square (phase after this tick's increment)
+    int nx = cx + pxp, ny = cy + pyp;
+    if (color == 2 && inside(c, nx, ny) && (square_flags(c, pl, v, nx, ny) & SQ_TLIGHT)) {
+      if (c.separate_cost) cost += c.tl_penalty; else reward -= c.tl_penalty;
+    }
+    if (f & SQ_ICE) {
+      used_ice = true;
+      if (pcg_double(ice) < c.ice_p) {
+        int a = (int)pcg_int(ice, 9);
+        pxp = ACCX[a];
+        pyp = ACCY[a];
+      }
+    }
+    if (f & SQ_BROKEN) {
+      used_broken = true;
+      if (pcg_double(broken) < c.broken_p) v.flags |= kFlagFlatTire;
+    }
+    if (f & SQ_SAND) {
+      used_sand = true;
+      if (pcg_double(sand) < c.sand_p) {
+        cx += pxp;
+        cy += pyp;
+        v.vx = v.vy = 0;
+        break;
+      }
+    }
+    cx += pxp;
+    cy += pyp;
+  }
+  (void)gl_t;
+  (void)gl_d;
+  if (used_ice) stream_store_state(S.ice, i, ice);
+  if (used_broken) stream_store_state(S.broken, i, broken);
+  if (used_sand) stream_store_state(S.sand, i, sand);
+  if (v.flags & kFlagFlatTire) v.vx = v.vy = 0;
+  const bool accel = !(ax == 0 && ay == 0);
+  if (S.visited) {
+    uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
+    int b = (cx + 2) * c.vis_pitch + (cy + 2);
+    if (c.visited_penalty != 0.0 && accel && ((vis[b >> 5] >> (b & 31)) & 1u)) {
+      if (c.separate_cost) cost += c.visited_penalty; else reward -= c.visited_penalty;
+    }
+    vis[b >> 5] |= 1u << (b & 31);
+  }
+  const int ox = v.px, oy = v.py;
+  v.px = cx;
+  v.py = cy;
+  if (c.still_penalty != 0.0 && !accel && ox == cx && oy == cy) {
+    if (c.separate_cost) cost += c.still_penalty; else reward -= c.still_penalty;
+  }
+  v.elapsed += 1u;
+  if (c.max_steps > 0 && (int)v.elapsed >= c.max_steps) v.flags |= kFlagTruncated;
+  res.reward = c.separate_cost ? perf : reward;
+  res.cost = cost;
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// cooperative observation writer: the workgroup's contiguous [nb][obs_bytes] slice, 16-B stores
+// ------------------------------------------------------------------------------------------------
+__device__ void write_obs_block(const DevCfg& c, uint8_t* __restrict__ dst, uint64_t env0, int nb,
+                                const uint32_t* __restrict__ masks, int mstride, const uint8_t* __restrict__ sel) {
+  const int OB = c.obs_bytes, MW = c.mask_words, WW = c.win * c.win;
+  uint8_t* base = dst + env0 * (uint64_t)OB;
+  const uint64_t total = (uint64_t)nb * OB;
+  const uintptr_t a0 = (uintptr_t)base, a1 = a0 + total;
+  const uintptr_t c0 = a0 & ~(uintptr_t)15;
+  const uint64_t nchunks = (a1 - c0 + 15) >> 4;
+  for (uint64_t ch = threadIdx.x; ch < nchunks; ch += blockDim.x) {
+    uintptr_t ca = c0 + (ch << 4);
+    uint8_t bytes[16];
+    bool full = true, any = false;
+    int64_t r = (int64_t)(ca - a0);
+    // decompose the first byte's offset once, then walk
+    int e = 0, rem = 0;
+    if (r >= 0) {
+      e = (int)(r / OB);
+      rem = (int)(r - (int64_t)e * OB);
+    }
+    int ci = rem / WW, sq = rem - ci * WW;
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+      int64_t rb = r + b;
+      uint8_t val = 0;
+      bool in = rb >= 0 && (uint64_t)rb < total && (sel == nullptr || sel[rb >= 0 ? e : 0]);
+      if (in) {
+        const uint32_t* m = masks + e * mstride + ci * MW;
+        val = (uint8_t)((m[sq >> 5] >> (sq & 31)) & 1u);
+        any = true;
+      } else {
+        full = false;
+      }
+      bytes[b] = val;
+      if (rb >= 0) {  // advance (e, ci, sq)
+        if (++sq == WW) {
+          sq = 0;
+          if (++ci == c.n_channels) {
+            ci = 0;
+            ++e;
+          }
+        }
+      }
+    }
+    if (full) {
+      uint4 w;
+      w.x = bytes[0] | bytes[1] << 8 | bytes[2] << 16 | (uint32_t)bytes[3] << 24;
+      w.y = bytes[4] | bytes[5] << 8 | bytes[6] << 16 | (uint32_t)bytes[7] << 24;
+      w.z = bytes[8] | bytes[9] << 8 | bytes[10] << 16 | (uint32_t)bytes[11] << 24;
+      w.w = bytes[12] | bytes[13] << 8 | bytes[14] << 16 | (uint32_t)bytes[15] << 24;
+      *reinterpret_cast<uint4*>(ca) = w;
+    } else if (any) {
+      int64_t rr = r;
+      int ee = e;
+      (void)ee;
+      for (int b = 0; b < 16; b++) {
+        int64_t rb = rr + b;
+        if (rb < 0 || (uint64_t)rb >= total) continue;
+        int eb = (int)(rb / OB);
+        if (sel != nullptr && !sel[eb]) continue;
+        reinterpret_cast<uint8_t*>(ca)[b] = bytes[b];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------------
+struct Lds {
+  int plan_stride_dw;  // per-lane plan words (odd)
+  int scratch_dw;      // per-lane BFS scratch words (odd)
+  int mask_stride;     // per-lane obs mask words (odd)
+};
+
+__host__ __device__ inline int odd_up(int x) { return x | 1; }
+
+__host__ inline Lds lds_layout(const DevCfg& c) {
+  Lds l;
+  l.plan_stride_dw = odd_up((c.nt + 1) / 2);
+  l.scratch_dw = odd_up((2 * c.nt + 3) / 4);
+  l.mask_stride = odd_up(c.n_channels * c.mask_words);
+  return l;
+}
+__host__ inline size_t lds_bytes(const Lds& l) {
+  return (size_t)kBlock * 4 * (l.plan_stride_dw + l.scratch_dw + l.mask_stride) + kBlock * 2;
+}
+
+enum { MODE_STEP = 0, MODE_RESET_SEEDED = 1, MODE_RESET_UNSEEDED = 2, MODE_OBSERVE = 3 };
+
+__device__ __forceinline__ void write_small_outputs(const DevCfg& c, const PgtgOutputs& o, uint64_t i, const EnvView& v,
+                                                    const ObsInfo& oi, bool final) {
+  if (!final) {
+    if (o.position) reinterpret_cast<int2*>(o.position)[i] = make_int2(oi.posx, oi.posy);
+    if (o.velocity) reinterpret_cast<int2*>(o.velocity)[i] = make_int2(v.vx, v.vy);
+    if (o.next_subgoal) o.next_subgoal[i] = oi.nsd;
+  } else {
+    if (o.final_position) reinterpret_cast<int2*>(o.final_position)[i] = make_int2(oi.posx, oi.posy);
+    if (o.final_velocity) reinterpret_cast<int2*>(o.final_velocity)[i] = make_int2(v.vx, v.vy);
+    if (o.final_next_subgoal) o.final_next_subgoal[i] = oi.nsd;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, DevState S,
+                                                 const uint8_t* __restrict__ actions, const uint8_t* __restrict__ mask,
+                                                 PgtgOutputs out, int mode, Lds L) {
+  extern __shared__ uint32_t lds[];
+  const DevCfg& c = *cfg;
+  const int tid = threadIdx.x;
+  const uint64_t env0 = (uint64_t)blockIdx.x * kBlock;
+  const int nb = (int)min((uint64_t)kBlock, S.n - env0);
+  const uint64_t i = env0 + tid;
+  const bool live = tid < nb;
+  uint32_t* plan_w = lds + tid * L.plan_stride_dw;
+  uint32_t* scr_w = lds + kBlock * L.plan_stride_dw + tid * L.scratch_dw;
+  uint32_t* masks_all = lds + kBlock * (L.plan_stride_dw + L.scratch_dw);
+  uint32_t* masks = masks_all + tid * L.mask_stride;
+  uint8_t* sel = reinterpret_cast<uint8_t*>(masks_all + kBlock * L.mask_stride);  // [kBlock] terminal flags
+  Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
+  uint8_t* q = reinterpret_cast<uint8_t*>(scr_w);
+  uint8_t* par = q + c.nt;
+
+  EnvView v{};
+  bool done = false;
+  int err = 0;
+  StepResult res{0.0, 0.0};
+  if (live) {
+    v = rec_load(S.rec, i);
+    // stage the tile plan (16-B vector loads) into this lane's LDS slot
+    const uint4* src = reinterpret_cast<const uint4*>(S.plan + i * (uint64_t)c.plan_stride);
+    for (int k = 0; k < c.plan_stride / 8; k++) {
+      uint4 w4 = src[k];
+      uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (k * 4 + j < L.plan_stride_dw) plan_w[k * 4 + j] = wv[j];
+    }
+    bool do_reset = false;
+    if (mode == MODE_STEP) {
+      err = env_step(c, S, i, v, pl, actions[i], res);
+      done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
+    } else if (mode == MODE_RESET_SEEDED || mode == MODE_RESET_UNSEEDED) {
+      do_reset = mask == nullptr || mask[i] != 0;
+      if (do_reset && mode == MODE_RESET_SEEDED) v.spawn = 0;
+    }
+    if (mode == MODE_STEP) {
+      if (out.reward) out.reward[i] = res.reward;
+      if (out.cost) out.cost[i] = res.cost;
+      if (out.terminated) out.terminated[i] = (v.flags & kFlagTerminated) ? 1 : 0;
+      if (out.truncated) out.truncated[i] = (v.flags & kFlagTruncated) ? 1 : 0;
+      if (out.braking) out.braking[i] = (v.flags & kFlagBraking) ? 1 : 0;
+    }
+    (void)do_reset;
+    sel[tid] = (mode == MODE_STEP && done && c.autoreset && err == 0) ? 1 : 0;
+    if (mode == MODE_RESET_SEEDED || mode == MODE_RESET_UNSEEDED) sel[tid] = do_reset ? 2 : 0;
+  }
+  __syncthreads();
+  const bool any_final = __syncthreads_or(live && sel[tid] == 1);
+  if (mode == MODE_STEP && any_final && (out.final_obs || out.final_position)) {
+    // terminal observation of the envs that finished (gymnasium info["final_observation"])
+    ObsInfo oi;
+    if (live && sel[tid] == 1) {
+      build_obs(c, S, pl, v, masks, oi);
+      write_small_outputs(c, out, i, v, oi, true);
+    }
+    __syncthreads();
+    if (out.final_obs) write_obs_block(c, out.final_obs, env0, nb, masks_all, L.mask_stride, sel);
+    __syncthreads();
+  }
+  const bool reset_now = live && ((sel[tid] == 1) || (sel[tid] == 2));
+  const int n_resets = __syncthreads_count(reset_now);
+  if (tid == 0 && n_resets) atomicAdd(&S.counters[1], (unsigned long long)n_resets);
+  if (live) {
+    if (reset_now) {
+      int e2 = env_reset(c, S, i, v, pl.p, q, par);
+      if (e2) err = e2;
+      // persist the new plan
+      uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
+      for (int k = 0; k < c.plan_stride / 8; k++) {
+        uint32_t wv[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) wv[j] = (k * 4 + j < L.plan_stride_dw) ? plan_w[k * 4 + j] : 0u;
+        dstp[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      }
+    }
+    ObsInfo oi;
+    build_obs(c, S, pl, v, masks, oi);
+    write_small_outputs(c, out, i, v, oi, false);
+    if (mode != MODE_OBSERVE) rec_store(S.rec, i, v);
+    S.err[i] = (uint8_t)(-err);
+  }
+  __syncthreads();
+  if (out.obs) write_obs_block(c, out.obs, env0, nb, masks_all, L.mask_stride, nullptr);
+  if (mode == MODE_STEP && tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
+}
+
+__global__ void k_random_actions(uint8_t* a, uint64_t n, uint64_t seed, uint64_t t) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // splitmix64 of (seed, t, i) -> Lemire multiply-shift to [0, 9)
+  uint64_t z = seed ^ (t * 0x9E3779B97F4A7C15ull) ^ (i * 0xD1B54A32D192ED03ull);
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  a[i] = (uint8_t)(((z >> 32) * 9ull) >> 32);
+}
+
+__global__ void k_fill_seeds(uint64_t* seed, uint64_t n, uint64_t base, uint64_t offset) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) seed[i] = base + offset + i;
+}
+
+}  // namespace pgtg
+
+// ==================================================================================================
+// host side: config derivation + C ABI
+// ==================================================================================================
+using namespace pgtg;
+
+struct pgtg_handle {
+  int device = 0;
+  uint64_t n = 0;
+  hipStream_t stream = nullptr;
+  DevCfg hcfg{};
+  DevCfg* dcfg = nullptr;
+  DevState S{};
+  PgtgOutputs out{};
+  Lds L{};
+  size_t lds = 0;
+  std::vector<void*> allocs;
+  std::string err;
+  uint64_t seed_offset = 0;  // global index of env 0 (for sharded runs)
+  bool timing = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+};
+
+static thread_local std::string g_create_err;
+
+#define HIPCHK(h, x)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      (h)->err = std::string(#x) + ": " + hipGetErrorString(e_);                     \
+      return PGTG_E_DEVICE;                                                          \
+    }                                                                                \
+  } while (0)
+
+template <typename T>
+static int dalloc(pgtg_handle* h, T** p, size_t count) {
+  void* q = nullptr;
+  if (count == 0) count = 1;
+  HIPCHK(h, hipMalloc(&q, count * sizeof(T)));
+  HIPCHK(h, hipMemset(q, 0, count * sizeof(T)));
+  h->allocs.push_back(q);
+  *p = reinterpret_cast<T*>(q);
+  return 0;
+}
+
+static int fail(pgtg_handle* h, int code, const std::string& m) {
+  h->err = m;
+  return code;
+}
+
+// atan2 octant tables (host libm == CPython math.atan2) ---------------------------------------
+static int8_t nsd_dir(int dx, int dy) {  // environment.py:1483-1502
+  double angle = atan2(-(double)dy, (double)dx);
+  double q = (angle + M_PI) / (M_PI / 4);
+  double mq = fmod(q, 8.0);
+  if (mq < 0) mq += 8.0;
+  static const int remap[8] = {2, 1, 0, 7, 6, 5, 4, 3};
+  return (int8_t)remap[(int)mq];
+}
+static int8_t compass_dir(int dx, int dy, int s) {  // environment.py:1058-1090
+  if (abs(dx) <= s && abs(dy) <= s) return -1;
+  double angle = atan2((double)dy, (double)dx);
+  double P8 = M_PI / 8;
+  if (-P8 <= angle && angle < P8) return 2;
+  if (P8 <= angle && angle < 3 * P8) return 3;
+  if (3 * P8 <= angle && angle < 5 * P8) return 4;
+  if (5 * P8 <= angle && angle < 7 * P8) return 5;
+  if (angle >= 7 * P8 || angle < -7 * P8) return 6;
+  if (-7 * P8 <= angle && angle < -5 * P8) return 7;
+  if (-5 * P8 <= angle && angle < -3 * P8) return 0;
+  if (-3 * P8 <= angle && angle < -P8) return 1;
+  return -1;
+}
+
+static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
+  memset(&c, 0, sizeof c);
+  if (in.abi_version != PGTG_ABI_VERSION) return fail(h, PGTG_E_INVALID, "ABI version mismatch");
+  int tw = in.fixed_map ? in.fm_w : in.width, th = in.fixed_map ? in.fm_h : in.height;
+  if (tw < 1 || th < 1) return fail(h, PGTG_E_INVALID, "map width and height must be >= 1");
+  if (tw * th > PGTG_MAX_TILES) return fail(h, PGTG_E_UNSUPPORTED, "this build supports width*height <= 64 tiles");
+  c.tw = tw;
+  c.th = th;
+  c.nt = tw * th;
+  c.W = tw * kTile;
+  c.H = th * kTile;
+  c.fixed_map = in.fixed_map;
+  if (in.fixed_map) {
+    for (int t = 0; t < c.nt; t++) {
+      uint32_t p = in.fm_exits[t] & 15u;
+      if (in.fm_obst_type[t] >= 0) p |= (uint32_t)(in.fm_obst_type[t] + 1) << 4 | (uint32_t)in.fm_obst_mask[t] << 7;
+      c.fixed_plan[t] = (uint16_t)p;
+    }
+    int st = in.fm_start[1] * tw + in.fm_start[0], gl = in.fm_goal[1] * tw + in.fm_goal[0];
+    if (in.fm_start[0] < 0 || in.fm_start[0] >= tw || in.fm_start[1] < 0 || in.fm_start[1] >= th || in.fm_goal[0] < 0 ||
+        in.fm_goal[0] >= tw || in.fm_goal[1] < 0 || in.fm_goal[1] >= th)
+      return fail(h, PGTG_E_INVALID, "fixed map start/goal outside the map");
+    c.fixed_sg = (uint32_t)st | (uint32_t)in.fm_start[2] << 8 | (uint32_t)gl << 16 | (uint32_t)in.fm_goal[2] << 24;
+  }
+  c.start_mode = in.start_mode;
+  c.goal_mode = in.goal_mode;
+  c.sx = in.start_x;
+  c.sy = in.start_y;
+  c.sdir = in.start_dir;
+  c.gx = in.goal_x;
+  c.gy = in.goal_y;
+  c.gdir = in.goal_dir;
+  c.min_distance = in.min_distance;
+  // removable_edges in graph-theory nested-dict order (map_generator.py:218-227): sources keyed in
+  // first-use order while adding (x,y)-(x+1,y) and (x,y)-(x,y+1) bidirectionally, x outer, y inner.
+  {
+    std::vector<int> keys;
+    std::vector<std::vector<int>> dst(c.nt);
+    std::vector<int> seen(c.nt, 0);
+    auto add1 = [&](int a, int b) {
+      if (!seen[a]) {
+        seen[a] = 1;
+        keys.push_back(a);
+      }
+      dst[a].push_back(b);
+    };
+    for (int x = 0; x < tw; x++)
+      for (int y = 0; y < th; y++) {
+        int t = y * tw + x;
+        if (x < tw - 1) {
+          add1(t, t + 1);
+          add1(t + 1, t);
+        }
+        if (y < th - 1) {
+          add1(t, t + tw);
+          add1(t + tw, t);
+        }
+      }
+    int n = 0;
+    for (int a : keys)
+      for (int b : dst[a]) {
+        c.ea[n] = (uint8_t)a;
+        c.eb[n] = (uint8_t)b;
+        c.ed[n] = (uint8_t)(b == a - tw ? 0 : b == a + 1 ? 1 : b == a + tw ? 2 : 3);
+        n++;
+      }
+    c.n_edges = n;
+    for (int e = 0; e < n; e++)
+      for (int f = 0; f < n; f++)
+        if (c.ea[f] == c.eb[e] && c.eb[f] == c.ea[e]) c.erev[e] = (uint8_t)f;
+    c.keep = (int)nearbyint((double)n * in.pct_connections);  // Python round (half to even)
+  }
+  // border candidates (map_generator.py:352-364)
+  {
+    std::vector<std::array<int, 3>> L;
+    for (int x = 0; x < tw; x++) L.push_back({0, x, 0});
+    for (int y = 0; y < th; y++) L.push_back({y, tw - 1, 1});
+    for (int x = 0; x < tw; x++) L.push_back({th - 1, x, 2});
+    for (int y = 0; y < th; y++) L.push_back({y, 0, 3});
+    std::array<int, 3> rm[2] = {{th - 1, 0, 3}, {0, tw - 1, 1}};
+    for (auto& r : rm)
+      for (size_t i = 0; i < L.size(); i++)
+        if (L[i] == r) {
+          L.erase(L.begin() + i);
+          break;
+        }
+    if ((int)L.size() > kMaxBorder) return fail(h, PGTG_E_UNSUPPORTED, "too many border connections");
+    c.n_border = (int)L.size();
+    for (size_t i = 0; i < L.size(); i++) {
+      c.bt[i] = (uint8_t)(L[i][0] * tw + L[i][1]);
+      c.bd[i] = (uint8_t)L[i][2];
+    }
+    c.n_border_add = (int)nearbyint((double)L.size() * in.pct_connections);
+  }
+  c.obstacle_probability = in.obstacle_probability;
+  {
+    double ws = in.w_ice + in.w_broken + in.w_sand + in.w_tl;
+    double p[4] = {in.w_ice / ws, in.w_broken / ws, in.w_sand / ws, in.w_tl / ws};
+    double acc = 0.0, cdf[4];
+    for (int k = 0; k < 4; k++) {
+      acc += p[k];
+      cdf[k] = acc;
+    }
+    for (int k = 0; k < 4; k++) c.obst_cdf[k] = cdf[k] / cdf[3];
+  }
+  c.ice_p = in.ice_probability;
+  c.broken_p = in.street_damage_probability;
+  c.sand_p = in.sand_probability;
+  c.phase_total = in.phase_dur[0] + in.phase_dur[1] + in.phase_dur[2];
+  if (c.phase_total <= 0 || c.phase_total > 65535) return fail(h, PGTG_E_INVALID, "invalid traffic light phases");
+  c.phase_g = in.phase_dur[0];
+  c.phase_gy = in.phase_dur[0] + in.phase_dur[1];
+  c.ignore_collisions = in.ignore_traffic_collisions;
+  c.separate_cost = in.separate_reward_cost;
+  c.autoreset = in.autoreset;
+  c.max_steps = in.max_episode_steps;
+  c.crash_penalty = in.crash_penalty;
+  c.final_goal_bonus = in.final_goal_bonus;
+  c.tl_penalty = in.tl_violation_penalty;
+  c.still_penalty = in.standing_still_penalty;
+  c.visited_penalty = in.visited_penalty;
+  for (int k = 1; k <= kMaxTiles; k++) c.ind_reward[k] = in.sum_subgoals_reward / (double)k;
+  c.n_channels = in.n_channels;
+  if (c.n_channels < 0 || c.n_channels > PGTG_MAX_CHANNELS) return fail(h, PGTG_E_INVALID, "bad channel count");
+  c.sliding = in.sliding;
+  c.ss = in.sliding_size;
+  c.win = in.sliding ? 1 + 2 * in.sliding_size : kTile;
+  if (c.win < 1 || c.win > kMaxWin) return fail(h, PGTG_E_UNSUPPORTED, "observation window larger than 15");
+  c.next_subgoal = in.next_subgoal;
+  c.generic_channels = 0;
+  for (int k = 0; k < c.n_channels; k++) {
+    c.channels[k] = in.channels[k];
+    if (in.channels[k] == PGTG_CH_SPAWNER || in.channels[k] >= PGTG_CH_LANE0) c.generic_channels = 1;
+  }
+  c.mask_words = (c.win * c.win + 31) / 32;
+  c.obs_bytes = c.n_channels * c.win * c.win;
+  // streams that can ever be drawn from (unobservable streams are never materialised)
+  bool obst_possible = in.fixed_map ? false : in.obstacle_probability > 0;
+  bool kinds[4] = {false, false, false, false};
+  if (in.fixed_map) {
+    for (int t = 0; t < c.nt; t++)
+      if (in.fm_obst_type[t] >= 0) kinds[in.fm_obst_type[t]] = true;
+  } else if (obst_possible) {
+    double w[4] = {in.w_ice, in.w_broken, in.w_sand, in.w_tl};
+    for (int k = 0; k < 4; k++) kinds[k] = w[k] > 0;
+  }
+  c.need_ice = kinds[0];
+  c.need_broken = kinds[1];
+  c.need_sand = kinds[2];
+  c.density = in.traffic_density;
+  c.need_car = in.traffic_density > 0;
+  if (c.need_car) return fail(h, PGTG_E_UNSUPPORTED, "traffic is not enabled in this build yet");
+  {
+    double tot = 0.0, p[5];
+    for (int k = 0; k < 5; k++) tot += in.profile_pct[k];
+    for (int k = 0; k < 5; k++) p[k] = tot > 0 ? in.profile_pct[k] / tot : (k == 1 ? 1.0 : 0.0);
+    double acc = 0.0, cdf[5];
+    for (int k = 0; k < 5; k++) {
+      acc += p[k];
+      cdf[k] = acc;
+    }
+    for (int k = 0; k < 5; k++) c.profile_cdf[k] = cdf[k] / cdf[4];
+  }
+  c.n_rules = in.n_rules;
+  for (int k = 0; k < in.n_rules && k < PGTG_MAX_RULES; k++) c.rules[k] = in.rules[k];
+  c.nsd_off = c.W > c.H ? c.W : c.H;
+  c.nsd_pitch = 2 * c.nsd_off + 1;
+  c.cmp_off = c.nsd_off + 2;
+  c.cmp_pitch = 2 * c.cmp_off + 1;
+  c.vis_pitch = c.H + 4;
+  c.vis_words = ((c.W + 4) * (c.H + 4) + 31) / 32;
+  c.plan_stride = ((c.nt + 7) / 8) * 8;
+  return 0;
+}
+
+extern "C" {
+
+int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_handle** out) {
+  if (!cfg || !out) return PGTG_E_INVALID;
+  pgtg_handle* h = new pgtg_handle();
+  *out = nullptr;
+  h->device = device;
+  h->n = n_envs;
+  int rc = 0;
+  if (n_envs == 0) rc = fail(h, PGTG_E_INVALID, "n_envs must be > 0");
+  if (!rc) rc = derive_cfg(h, *cfg, h->hcfg);
+  if (rc) {
+    g_create_err = h->err;
+    delete h;
+    return rc;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    g_create_err = "hipSetDevice failed";
+    delete h;
+    return PGTG_E_DEVICE;
+  }
+  const DevCfg& c = h->hcfg;
+  DevState& S = h->S;
+  S.n = n_envs;
+  uint64_t n = n_envs;
+#define ALLOC(p, cnt)                 \
+  if ((rc = dalloc(h, &(p), (cnt)))) { \
+    g_create_err = h->err;            \
+    pgtg_destroy(h);                  \
+    return rc;                        \
+  }
+  ALLOC(h->dcfg, 1);
+  ALLOC(S.rec, n);
+  ALLOC(S.seed, n);
+  ALLOC(S.plan, n * (uint64_t)c.plan_stride);
+  ALLOC(S.err, n);
+  ALLOC(S.counters, 2);
+  DevStream* streams[4] = {&S.car, &S.ice, &S.broken, &S.sand};
+  int needs[4] = {c.need_car, c.need_ice, c.need_broken, c.need_sand};
+  for (int k = 0; k < 4; k++)
+    if (needs[k]) {
+      ALLOC(streams[k]->shi, n);
+      ALLOC(streams[k]->slo, n);
+      ALLOC(streams[k]->ihi, n);
+      ALLOC(streams[k]->ilo, n);
+      ALLOC(streams[k]->buf, n);
+    }
+  if (c.visited_penalty != 0.0) ALLOC(S.visited, n * (uint64_t)c.vis_words);
+  // atan2 tables
+  {
+    std::vector<int8_t> nsd((size_t)c.nsd_pitch * c.nsd_pitch), cmp((size_t)c.cmp_pitch * c.cmp_pitch);
+    for (int a = 0; a < c.nsd_pitch; a++)
+      for (int b = 0; b < c.nsd_pitch; b++) nsd[(size_t)a * c.nsd_pitch + b] = nsd_dir(a - c.nsd_off, b - c.nsd_off);
+    for (int a = 0; a < c.cmp_pitch; a++)
+      for (int b = 0; b < c.cmp_pitch; b++)
+        cmp[(size_t)a * c.cmp_pitch + b] = compass_dir(a - c.cmp_off, b - c.cmp_off, cfg->sliding_size);
+    int8_t *dn = nullptr, *dc = nullptr;
+    ALLOC(dn, nsd.size());
+    ALLOC(dc, cmp.size());
+    if (hipMemcpy(dn, nsd.data(), nsd.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dc, cmp.data(), cmp.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      g_create_err = "table upload failed";
+      pgtg_destroy(h);
+      return PGTG_E_DEVICE;
+    }
+    S.nsd_tab = dn;
+    S.cmp_tab = dc;
+  }
+#undef ALLOC
+  if (hipMemcpy(h->dcfg, &h->hcfg, sizeof(DevCfg), hipMemcpyHostToDevice) != hipSuccess) {
+    g_create_err = "config upload failed";
+    pgtg_destroy(h);
+    return PGTG_E_DEVICE;
+  }
+  h->L = lds_layout(c);
+  h->lds = lds_bytes(h->L);
+  if (h->lds > 160 * 1024) {
+    g_create_err = "LDS budget exceeded";
+    pgtg_destroy(h);
+    return PGTG_E_UNSUPPORTED;
+  }
+  if (h->lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)k_env, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+  *out = h;
+  return PGTG_OK;
+}
+
+int pgtg_destroy(pgtg_handle* h) {
+  if (!h) return PGTG_OK;
+  for (void* p : h->allocs) (void)hipFree(p);
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  delete h;
+  return PGTG_OK;
+}
+
+int pgtg_set_stream(pgtg_handle* h, void* stream) {
+  if (!h) return PGTG_E_INVALID;
+  h->stream = reinterpret_cast<hipStream_t>(stream);
+  return PGTG_OK;
+}
+
+int pgtg_set_outputs(pgtg_handle* h, const PgtgOutputs* o) {
+  if (!h || !o) return PGTG_E_INVALID;
+  h->out = *o;
+  return PGTG_OK;
+}
+
+static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, int mode) {
+  HIPCHK(h, hipSetDevice(h->device));
+  uint64_t blocks = (h->n + kBlock - 1) / kBlock;
+  if (h->timing && mode == MODE_STEP) {
+    if (!h->ev0) {
+      HIPCHK(h, hipEventCreate(&h->ev0));
+      HIPCHK(h, hipEventCreate(&h->ev1));
+    }
+    HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+  }
+  hipLaunchKernelGGL(k_env, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->S, actions, mask,
+                     h->out, mode, h->L);
+  HIPCHK(h, hipGetLastError());
+  if (h->timing && mode == MODE_STEP) {
+    HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+    h->timed = true;
+  }
+  return PGTG_OK;
+}
+
+int pgtg_reset(pgtg_handle* h, const uint64_t* seeds_host, uint64_t seed_base, const uint8_t* mask_dev) {
+  if (!h) return PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  if (seeds_host) {
+    HIPCHK(h, hipMemcpyAsync(h->S.seed, seeds_host, h->n * sizeof(uint64_t), hipMemcpyHostToDevice, h->stream));
+  } else {
+    hipLaunchKernelGGL(k_fill_seeds, dim3((unsigned)((h->n + 255) / 256)), dim3(256), 0, h->stream, h->S.seed, h->n,
+                       seed_base, (uint64_t)0);
+    HIPCHK(h, hipGetLastError());
+  }
+  return launch(h, nullptr, mask_dev, MODE_RESET_SEEDED);
+}
+
+int pgtg_reset_unseeded(pgtg_handle* h, const uint8_t* mask_dev) {
+  if (!h) return PGTG_E_INVALID;
+  return launch(h, nullptr, mask_dev, MODE_RESET_UNSEEDED);
+}
+
+int pgtg_step(pgtg_handle* h, const uint8_t* actions_dev) {
+  if (!h || !actions_dev) return PGTG_E_INVALID;
+  return launch(h, actions_dev, nullptr, MODE_STEP);
+}
+
+int pgtg_observe(pgtg_handle* h) {
+  if (!h) return PGTG_E_INVALID;
+  return launch(h, nullptr, nullptr, MODE_OBSERVE);
+}
+
+int pgtg_random_actions(pgtg_handle* h, uint8_t* actions_dev, uint64_t seed, uint64_t t) {
+  if (!h || !actions_dev) return PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  hipLaunchKernelGGL(k_random_actions, dim3((unsigned)((h->n + 255) / 256)), dim3(256), 0, h->stream, actions_dev, h->n,
+                     seed, t);
+  HIPCHK(h, hipGetLastError());
+  return PGTG_OK;
+}
+
+int pgtg_get_env_state(pgtg_handle* h, uint64_t env, PgtgEnvState* st) {
+  if (!h || !st || env >= h->n) return PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  EnvRec r;
+  uint64_t seed;
+  uint8_t e;
+  HIPCHK(h, hipMemcpy(&r, h->S.rec + env, sizeof r, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(&seed, h->S.seed + env, sizeof seed, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(&e, h->S.err + env, 1, hipMemcpyDeviceToHost));
+  memset(st, 0, sizeof *st);
+  st->x = (int16_t)(r.a.x & 0xffffu);
+  st->y = (int16_t)(r.a.x >> 16);
+  st->vx = (int16_t)(r.a.y & 0xffffu);
+  st->vy = (int16_t)(r.a.y >> 16);
+  st->phase = (int)(r.a.z & 0xffffu);
+  uint32_t fl = (r.a.z >> 16) & 0xffu;
+  st->terminated = (fl & kFlagTerminated) ? 1 : 0;
+  st->flat_tire = (fl & kFlagFlatTire) ? 1 : 0;
+  st->path_len = (int)(r.a.z >> 24);
+  st->elapsed = (int)r.a.w;
+  st->spawn_counter = r.b.y;
+  st->used_subgoals = (uint64_t)r.b.z | ((uint64_t)r.b.w << 32);
+  st->seed = seed;
+  st->error = -(int)e;
+  return PGTG_OK;
+}
+
+int pgtg_get_cars(pgtg_handle* h, uint64_t env, PgtgCar* cars, int32_t cap, int32_t* n) {
+  if (!h || env >= h->n || !n) return PGTG_E_INVALID;
+  (void)cars;
+  (void)cap;
+  *n = 0;
+  return PGTG_OK;
+}
+
+int pgtg_get_map_plan(pgtg_handle* h, uint64_t env, int32_t* w, int32_t* h_, uint8_t* exits, int8_t* otype,
+                      int8_t* omask, int32_t* start3, int32_t* goal3) {
+  if (!h || env >= h->n) return PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const DevCfg& c = h->hcfg;
+  std::vector<uint16_t> p(c.plan_stride);
+  EnvRec r;
+  HIPCHK(h, hipMemcpy(p.data(), h->S.plan + env * (uint64_t)c.plan_stride, c.plan_stride * 2, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(&r, h->S.rec + env, sizeof r, hipMemcpyDeviceToHost));
+  *w = c.tw;
+  *h_ = c.th;
+  for (int t = 0; t < c.nt; t++) {
+    exits[t] = (uint8_t)plan_exits(p[t]);
+    int ot = (int)plan_otype(p[t]);
+    otype[t] = (int8_t)(ot - 1);
+    omask[t] = (int8_t)(ot ? (int)plan_omask(p[t]) : -1);
+  }
+  uint32_t sg = r.b.x;
+  start3[0] = (int)(sg & 0xffu) % c.tw;
+  start3[1] = (int)(sg & 0xffu) / c.tw;
+  start3[2] = (int)((sg >> 8) & 0xffu);
+  goal3[0] = (int)((sg >> 16) & 0xffu) % c.tw;
+  goal3[1] = (int)((sg >> 16) & 0xffu) / c.tw;
+  goal3[2] = (int)(sg >> 24);
+  return PGTG_OK;
+}
+
+int pgtg_set_agent(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t vx, int32_t vy) {
+  if (!h || env >= h->n) return PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  EnvRec r;
+  HIPCHK(h, hipMemcpy(&r, h->S.rec + env, sizeof r, hipMemcpyDeviceToHost));
+  r.a.x = ((uint32_t)x & 0xffffu) | ((uint32_t)y << 16);
+  r.a.y = ((uint32_t)vx & 0xffffu) | ((uint32_t)vy << 16);
+  HIPCHK(h, hipMemcpy(h->S.rec + env, &r, sizeof r, hipMemcpyHostToDevice));
+  return PGTG_OK;
+}
+
+int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t route, int32_t profile) {
+  if (!h) return PGTG_E_INVALID;
+  (void)env; (void)x; (void)y; (void)route; (void)profile;
+  return fail(h, PGTG_E_UNSUPPORTED, "traffic is not enabled in this build yet");
+}
+
+int pgtg_get_counters(pgtg_handle* h, uint64_t* env_steps, uint64_t* episodes) {
+  if (!h) return PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  unsigned long long c[2];
+  HIPCHK(h, hipMemcpy(c, h->S.counters, sizeof c, hipMemcpyDeviceToHost));
+  if (env_steps) *env_steps = c[0];
+  if (episodes) *episodes = c[1];
+  return PGTG_OK;
+}
+
+int pgtg_error_count(pgtg_handle* h, uint64_t* n_errors, int32_t* first_code) {
+  if (!h) return PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  std::vector<uint8_t> e(h->n);
+  HIPCHK(h, hipMemcpy(e.data(), h->S.err, h->n, hipMemcpyDeviceToHost));
+  uint64_t cnt = 0;
+  int first = 0;
+  for (uint64_t i = 0; i < h->n; i++)
+    if (e[i]) {
+      if (!cnt) first = -(int)e[i];
+      cnt++;
+    }
+  if (n_errors) *n_errors = cnt;
+  if (first_code) *first_code = first;
+  return PGTG_OK;
+}
+
+int pgtg_window(const pgtg_handle* h) { return h ? h->hcfg.win : 0; }
+uint64_t pgtg_num_envs(const pgtg_handle* h) { return h ? h->n : 0; }
+const char* pgtg_last_error(const pgtg_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
+
+int pgtg_enable_timing(pgtg_handle* h, int32_t on) {
+  if (!h) return PGTG_E_INVALID;
+  h->timing = on != 0;
+  return PGTG_OK;
+}
+
+float pgtg_last_step_ms(pgtg_handle* h) {
+  if (!h || !h->timed) return -1.f;
+  float ms = -1.f;
+  if (hipEventSynchronize(h->ev1) != hipSuccess) return -1.f;
+  if (hipEventElapsedTime(&ms, h->ev0, h->ev1) != hipSuccess) return -1.f;
+  return ms;
+}
+
+}  // extern "C"

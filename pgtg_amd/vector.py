@@ -1,0 +1,232 @@
+"""Batched, device-resident PGTG environments (the MI355X hot path).
+
+`PGTGVecEnv(num_envs, map_path=None, **PGTGEnv kwargs)` advances `num_envs` independent reference
+episodes in lockstep on one GPU through the C ABI (include/pgtg.h) of `libpgtg_hip.so`.  Semantics
+per env are the reference's `PGTGEnv.reset/step` (pgtg/environment.py:581-656, 1092-1281); the
+batch follows the gymnasium/SB3 vector-env conventions: env i of a `reset(seed=s)` is seeded with
+`s + i`, and an env that terminates (or is truncated by `max_episode_steps`, the TimeLimit wrapper
+of pgtg/train.py:39) is reset unseeded in the same step, its terminal observation being returned
+in `infos["final_observation"]`.
+
+All returned tensors live on the GPU and are views of handle-owned buffers, valid until the next
+call (clone them to keep them).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Any
+
+from . import _abi
+from .config import EnvSpec, make_spec
+
+_EXC = {
+    _abi.PGTG_E_INVALID: ValueError,
+    _abi.PGTG_E_DONE: RuntimeError,
+    _abi.PGTG_E_DEVICE: RuntimeError,
+    _abi.PGTG_E_UNSUPPORTED: ValueError,
+    _abi.PGTG_E_MAP: ValueError,
+}
+
+
+def _check(rc: int, handle=None) -> None:
+    if rc != _abi.PGTG_OK:
+        msg = _abi.lib().pgtg_last_error(handle)
+        raise _EXC.get(rc, RuntimeError)((msg or b"").decode() or f"pgtg error {rc}")
+
+
+class PGTGVecEnv:
+    def __init__(self, num_envs: int, map_path: str | None = None, *, device: int | None = None,
+                 autoreset: bool = True, max_episode_steps: int | None = None, spec: EnvSpec | None = None,
+                 **kwargs: Any):
+        import torch
+
+        self.spec = spec if spec is not None else make_spec(map_path, **kwargs)
+        self.num_envs = int(num_envs)
+        self.autoreset = autoreset
+        self.max_episode_steps = max_episode_steps
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device)
+        self._lib = _abi.lib()
+        self._cfg = _abi.config_struct(self.spec, autoreset, max_episode_steps)
+        h = C.c_void_p()
+        _check(self._lib.pgtg_create(C.byref(self._cfg), self.num_envs, int(device), C.byref(h)), None)
+        self._h = h
+        self.window = self._lib.pgtg_window(h)
+        self.keys = [k for k, _ in self.spec.channels]
+        N, Cn, W = self.num_envs, len(self.keys), self.window
+        dev = self.device
+        t = torch
+        self.obs_map = t.zeros((N, Cn, W, W), dtype=t.uint8, device=dev)
+        self.position = t.zeros((N, 2), dtype=t.int32, device=dev)
+        self.velocity = t.zeros((N, 2), dtype=t.int32, device=dev)
+        self.reward = t.zeros((N,), dtype=t.float64, device=dev)
+        self.terminated = t.zeros((N,), dtype=t.bool, device=dev)
+        self.truncated = t.zeros((N,), dtype=t.bool, device=dev)
+        self.braking = t.zeros((N,), dtype=t.bool, device=dev)
+        self.cost = t.zeros((N,), dtype=t.float64, device=dev) if self.spec.separate_reward_cost else None
+        self.nsd = t.full((N,), -1, dtype=t.int32, device=dev) if self.spec.next_subgoal else None
+        if autoreset:
+            self.final_map = t.zeros_like(self.obs_map)
+            self.final_position = t.zeros_like(self.position)
+            self.final_velocity = t.zeros_like(self.velocity)
+            self.final_nsd = t.full((N,), -1, dtype=t.int32, device=dev) if self.spec.next_subgoal else None
+        else:
+            self.final_map = self.final_position = self.final_velocity = self.final_nsd = None
+        self.actions = t.zeros((N,), dtype=t.uint8, device=dev)
+        o = _abi.PgtgOutputs()
+        ptr = lambda x: None if x is None else x.data_ptr()  # noqa: E731
+        o.obs, o.position, o.velocity = ptr(self.obs_map), ptr(self.position), ptr(self.velocity)
+        o.next_subgoal, o.reward, o.cost = ptr(self.nsd), ptr(self.reward), ptr(self.cost)
+        o.terminated, o.truncated, o.braking = ptr(self.terminated), ptr(self.truncated), ptr(self.braking)
+        o.final_obs, o.final_position = ptr(self.final_map), ptr(self.final_position)
+        o.final_velocity, o.final_next_subgoal = ptr(self.final_velocity), ptr(self.final_nsd)
+        self._outs = o
+        _check(self._lib.pgtg_set_outputs(h, C.byref(o)), h)
+        self._seeded = False
+
+    # -- plumbing ------------------------------------------------------------------------------
+    def _bind_stream(self):
+        import torch
+        s = torch.cuda.current_stream(self.device)
+        _check(self._lib.pgtg_set_stream(self._h, C.c_void_p(s.cuda_stream)), self._h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.pgtg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def observation(self) -> dict:
+        o = {"position": self.position, "velocity": self.velocity,
+             "map": {k: self.obs_map[:, i] for i, k in enumerate(self.keys)}}
+        if self.nsd is not None:
+            o["next_subgoal_direction"] = self.nsd
+        return o
+
+    def final_observation(self) -> dict:
+        o = {"position": self.final_position, "velocity": self.final_velocity,
+             "map": {k: self.final_map[:, i] for i, k in enumerate(self.keys)}}
+        if self.final_nsd is not None:
+            o["next_subgoal_direction"] = self.final_nsd
+        return o
+
+    # -- API -----------------------------------------------------------------------------------
+    def reset(self, *, seed: int | list[int] | None = None, options: dict | None = None,
+              mask=None) -> tuple[dict, dict]:
+        """Seeded reset: env i gets seed+i (or seed[i]); unseeded: next spawn block per env.
+        `mask` (bool/uint8 [N] tensor) restricts the reset to some envs."""
+        self._bind_stream()
+        mptr = None
+        if mask is not None:
+            import torch
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+            self._mask = m
+            mptr = C.c_void_p(m.data_ptr())
+        if seed is None and not self._seeded:
+            seed = int.from_bytes(os.urandom(7), "little")  # gymnasium: fresh OS entropy
+        if seed is None:
+            _check(self._lib.pgtg_reset_unseeded(self._h, mptr), self._h)
+        elif isinstance(seed, int):
+            if seed < 0:
+                raise ValueError("seed must be a non-negative int")
+            _check(self._lib.pgtg_reset(self._h, None, C.c_uint64(seed), mptr), self._h)
+        else:
+            seeds = (C.c_uint64 * self.num_envs)(*[int(s) for s in seed])
+            _check(self._lib.pgtg_reset(self._h, seeds, 0, mptr), self._h)
+        self._seeded = True
+        return self.observation(), {}
+
+    def step(self, actions) -> tuple[dict, Any, Any, Any, dict]:
+        import torch
+        self._bind_stream()
+        if not isinstance(actions, torch.Tensor):
+            actions = torch.as_tensor(actions)
+        a = actions
+        if a.device != self.device or a.dtype != torch.uint8:
+            a = a.to(device=self.device, dtype=torch.uint8)
+        a = a.contiguous()
+        self._act_ref = a
+        _check(self._lib.pgtg_step(self._h, C.c_void_p(a.data_ptr())), self._h)
+        if not self.autoreset:
+            self._raise_errors()
+        infos: dict[str, Any] = {"braking_applied": self.braking}
+        if self.autoreset:
+            done = self.terminated | self.truncated
+            infos["final_observation"] = self.final_observation()
+            infos["_final_observation"] = done
+        if self.cost is not None:
+            infos["cost"] = self.cost
+        return self.observation(), self.reward, self.terminated, self.truncated, infos
+
+    def step_random(self, seed: int, t: int):
+        """One tick with device-generated uniform random actions (synthetic rollouts, bench)."""
+        self._bind_stream()
+        _check(self._lib.pgtg_random_actions(self._h, C.c_void_p(self.actions.data_ptr()), C.c_uint64(seed),
+                                             C.c_uint64(t)), self._h)
+        _check(self._lib.pgtg_step(self._h, C.c_void_p(self.actions.data_ptr())), self._h)
+
+    def observe(self):
+        """Re-emit every env's observation (after set_agent / add_car)."""
+        self._bind_stream()
+        _check(self._lib.pgtg_observe(self._h), self._h)
+        return self.observation()
+
+    def _raise_errors(self):
+        n = C.c_uint64()
+        code = C.c_int32()
+        _check(self._lib.pgtg_error_count(self._h, C.byref(n), C.byref(code)), self._h)
+        if n.value:
+            if code.value == _abi.PGTG_E_DONE:
+                raise RuntimeError("Already done, step has no further effect")
+            raise _EXC.get(code.value, RuntimeError)(f"{n.value} env(s) failed with code {code.value}")
+
+    # -- introspection (host-synchronising) ------------------------------------------------------
+    def env_state(self, i: int) -> dict:
+        st = _abi.PgtgEnvState()
+        _check(self._lib.pgtg_get_env_state(self._h, i, C.byref(st)), self._h)
+        return {f: getattr(st, f) for f, _ in st._fields_}
+
+    def cars(self, i: int):
+        import numpy as np
+        n = C.c_int32()
+        _check(self._lib.pgtg_get_cars(self._h, i, None, 0, C.byref(n)), self._h)
+        arr = (_abi.PgtgCar * max(n.value, 1))()
+        _check(self._lib.pgtg_get_cars(self._h, i, arr, n.value, C.byref(n)), self._h)
+        return np.array([[c.id, c.x, c.y, c.route, c.profile, c.patience, c.delay] for c in arr[:n.value]],
+                        dtype=np.int32).reshape(n.value, 7)
+
+    def map_plan(self, i: int) -> dict:
+        w, h = C.c_int32(), C.c_int32()
+        ex = (C.c_uint8 * 64)()
+        ot = (C.c_int8 * 64)()
+        om = (C.c_int8 * 64)()
+        s3 = (C.c_int32 * 3)()
+        g3 = (C.c_int32 * 3)()
+        _check(self._lib.pgtg_get_map_plan(self._h, i, C.byref(w), C.byref(h), ex, ot, om, s3, g3), self._h)
+        n = w.value * h.value
+        return {"w": w.value, "h": h.value, "exits": list(ex[:n]), "otype": list(ot[:n]), "omask": list(om[:n]),
+                "start": tuple(s3), "goal": tuple(g3)}
+
+    def set_agent(self, i: int, x: int, y: int, vx: int, vy: int):
+        _check(self._lib.pgtg_set_agent(self._h, i, x, y, vx, vy), self._h)
+
+    def add_car(self, i: int, x: int, y: int, route: int, profile: int):
+        _check(self._lib.pgtg_add_car(self._h, i, x, y, route, profile), self._h)
+
+    def counters(self) -> tuple[int, int]:
+        a, b = C.c_uint64(), C.c_uint64()
+        _check(self._lib.pgtg_get_counters(self._h, C.byref(a), C.byref(b)), self._h)
+        return a.value, b.value
+
+    def enable_timing(self, on: bool = True):
+        self._lib.pgtg_enable_timing(self._h, int(on))
+
+    def last_step_ms(self) -> float:
+        return float(self._lib.pgtg_last_step_ms(self._h))

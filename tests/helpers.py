@@ -99,3 +99,79 @@ def replay_oracle(d: dict, n_envs: int | None = None, steps: int | None = None) 
             if len(bad) > 20:
                 return bad
     return bad
+
+
+def has_traffic(meta: dict) -> bool:
+    return float(meta["kwargs"].get("traffic_density", 0) or 0) > 0
+
+
+def replay_vec(d: dict, n_envs: int | None = None, steps: int | None = None) -> list[str]:
+    """Replay a golden trajectory through the HIP vector env (auto-reset); mismatch strings."""
+    import torch
+    from pgtg_amd.vector import PGTGVecEnv
+    meta = d["meta"]
+    spec = spec_for(meta)
+    perm = channel_perm(spec, meta["keys"])
+    N = meta["N"] if n_envs is None else min(n_envs, meta["N"])
+    T = meta["T"] if steps is None else min(steps, meta["T"])
+    env = PGTGVecEnv(N, spec=spec, autoreset=True)
+    bad: list[str] = []
+    obs, _ = env.reset(seed=meta["seed_base"])
+    torch.cuda.synchronize()
+    m = env.obs_map.cpu().numpy()[:, perm]
+    pos = env.position.cpu().numpy()
+    for i in range(N):
+        if not np.array_equal(m[i], d["init_obs"][i]):
+            bad.append(f"env{i} reset obs")
+        if tuple(pos[i]) != tuple(d["init_pos"][i]):
+            bad.append(f"env{i} reset pos {pos[i]} vs {d['init_pos'][i]}")
+        if spec.next_subgoal and int(env.nsd[i]) != int(d["init_nsd"][i]):
+            bad.append(f"env{i} reset nsd")
+    reset_map = {(int(t), int(i)): k for k, (t, i) in enumerate(d["reset_idx"])}
+    for t in range(T):
+        acts = torch.as_tensor(d["actions"][t, :N].astype(np.uint8)).cuda()
+        env.step(acts)
+        torch.cuda.synchronize()
+        m = env.obs_map.cpu().numpy()[:, perm]
+        fm = env.final_map.cpu().numpy()[:, perm]
+        pos, vel = env.position.cpu().numpy(), env.velocity.cpu().numpy()
+        fpos, fvel = env.final_position.cpu().numpy(), env.final_velocity.cpu().numpy()
+        rew, term = env.reward.cpu().numpy(), env.terminated.cpu().numpy()
+        trunc = env.truncated.cpu().numpy()
+        cost = env.cost.cpu().numpy() if env.cost is not None else np.zeros(N)
+        nsd = env.nsd.cpu().numpy() if env.nsd is not None else None
+        fnsd = env.final_nsd.cpu().numpy() if env.final_nsd is not None else None
+        for i in range(N):
+            tag = f"env{i} t{t}"
+            if bool(term[i]) != bool(d["terminated"][t, i]) or trunc[i]:
+                bad.append(f"{tag} terminated {term[i]} vs {d['terminated'][t, i]}")
+                continue
+            if rew[i] != d["reward"][t, i] or cost[i] != d["cost"][t, i]:
+                bad.append(f"{tag} reward {rew[i]} vs {d['reward'][t, i]} cost {cost[i]} vs {d['cost'][t, i]}")
+            if term[i]:
+                if not np.array_equal(fm[i], d["obs"][t, i]):
+                    bad.append(f"{tag} final obs")
+                if tuple(fpos[i]) != tuple(d["pos"][t, i]) or tuple(fvel[i]) != tuple(d["vel"][t, i]):
+                    bad.append(f"{tag} final pos/vel")
+                if fnsd is not None and fnsd[i] != d["nsd"][t, i]:
+                    bad.append(f"{tag} final nsd")
+                k = reset_map[(t, i)]
+                if not np.array_equal(m[i], d["reset_obs"][k]):
+                    bad.append(f"{tag} autoreset obs")
+                if tuple(pos[i]) != tuple(d["reset_pos"][k]):
+                    bad.append(f"{tag} autoreset pos")
+                if nsd is not None and nsd[i] != d["reset_nsd"][k]:
+                    bad.append(f"{tag} autoreset nsd")
+            else:
+                if not np.array_equal(m[i], d["obs"][t, i]):
+                    diff = [meta["keys"][c] for c in range(len(perm)) if not np.array_equal(m[i, c], d["obs"][t, i, c])]
+                    bad.append(f"{tag} obs {diff}")
+                if tuple(pos[i]) != tuple(d["pos"][t, i]) or tuple(vel[i]) != tuple(d["vel"][t, i]):
+                    bad.append(f"{tag} pos/vel {pos[i]} {vel[i]} vs {d['pos'][t, i]} {d['vel'][t, i]}")
+                if nsd is not None and nsd[i] != d["nsd"][t, i]:
+                    bad.append(f"{tag} nsd {nsd[i]} vs {d['nsd'][t, i]}")
+            if len(bad) > 30:
+                env.close()
+                return bad
+    env.close()
+    return bad
