@@ -171,9 +171,11 @@ int pgtg_error_count(pgtg_handle* h, uint64_t* n_errors, int32_t* first_code);
 int pgtg_window(const pgtg_handle* h);
 uint64_t pgtg_num_envs(const pgtg_handle* h);
 const char* pgtg_last_error(const pgtg_handle* h);
-/* Kernel timing of the last pgtg_step on the handle's stream (ms, HIP events); -1 if unavailable. */
-float pgtg_last_step_ms(pgtg_handle* h);
+/* Per-launch device timing of the step kernel with HIP events on the handle's stream.  When enabled,
+ * every pgtg_step brackets its kernel with an event pair; pgtg_timing_read synchronises and returns
+ * the summed kernel milliseconds and the number of timed launches (reset=1 clears the tally). */
 int pgtg_enable_timing(pgtg_handle* h, int32_t on);
+int pgtg_timing_read(pgtg_handle* h, double* total_ms, uint64_t* launches, int32_t reset);
 
 #ifdef __cplusplus
 }

@@ -105,6 +105,8 @@ def lib():
         L.orc_choice_p.restype = C.c_int64
         L.orc_choice_p.argtypes = [C.POINTER(OrcPcg), C.POINTER(C.c_double), C.c_int]
         L.orc_choice_noreplace.argtypes = [C.POINTER(OrcPcg), C.c_int64, C.c_int64, C.POINTER(C.c_int64)]
+        L.orc_bench.restype = C.c_int64
+        L.orc_bench.argtypes = [C.POINTER(OrcConfig), C.c_int, C.c_int, C.c_uint64, C.c_uint64]
         _lib = L
     return _lib
 
@@ -159,6 +161,15 @@ def config_from_spec(spec) -> OrcConfig:
             c.fm_start[i] = fm.start[i]
             c.fm_goal[i] = fm.goal[i]
     return c
+
+
+def bench(spec, n_envs: int, steps: int, seed_base: int = 0, act_seed: int = 12345) -> int:
+    """Run the oracle's built-in random-action rollout loop (bench.py cpu_baseline); env-steps done."""
+    c = config_from_spec(spec)
+    n = lib().orc_bench(C.byref(c), int(n_envs), int(steps), int(seed_base), int(act_seed))
+    if n < 0:
+        raise RuntimeError("oracle bench failed")
+    return n
 
 
 class OracleEnv:

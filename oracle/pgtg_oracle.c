@@ -1362,3 +1362,43 @@ int orc_get_squares(const orc_env* e, uint64_t* out, int cap) {
   for (int i = 0; i < n && i < cap; i++) out[i] = e->sq[i];
   return n;
 }
+
+/* CPU baseline leg of bench.py: n_envs envs, `steps` ticks each with uniform random actions from
+ * the same splitmix hash as the GPU action kernel, same-step auto-reset, like the vector env.
+ * Returns the number of env-steps executed (or -1). */
+int64_t orc_bench(const orc_config* cfg, int n_envs, int steps, uint64_t seed_base, uint64_t act_seed) {
+  int64_t done = 0;
+  int win = cfg->sliding ? 1 + 2 * cfg->sliding_size : TILE;
+  uint8_t* obs = (uint8_t*)malloc((size_t)cfg->n_channels * win * win + 1);
+  orc_out out;
+  for (int i = 0; i < n_envs; i++) {
+    orc_env* e = orc_create(cfg);
+    if (orc_reset(e, (int64_t)(seed_base + (uint64_t)i), obs, &out)) {
+      orc_destroy(e);
+      free(obs);
+      return -1;
+    }
+    for (int t = 0; t < steps; t++) {
+      uint64_t z = act_seed ^ ((uint64_t)t * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)i * 0xD1B54A32D192ED03ull);
+      z += 0x9E3779B97F4A7C15ull;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      z ^= z >> 31;
+      int a = (int)(((z >> 32) * 9ull) >> 32);
+      if (orc_step(e, a, obs, &out)) {
+        orc_destroy(e);
+        free(obs);
+        return -1;
+      }
+      done++;
+      if (out.terminated && orc_reset(e, -1, obs, &out)) {
+        orc_destroy(e);
+        free(obs);
+        return -1;
+      }
+    }
+    orc_destroy(e);
+  }
+  free(obs);
+  return done;
+}

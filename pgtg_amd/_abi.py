@@ -29,8 +29,8 @@ EXPORTED = [
     "pgtg_create", "pgtg_destroy", "pgtg_set_stream", "pgtg_set_outputs", "pgtg_reset",
     "pgtg_reset_unseeded", "pgtg_step", "pgtg_random_actions", "pgtg_get_env_state", "pgtg_get_cars",
     "pgtg_get_map_plan", "pgtg_set_agent", "pgtg_add_car", "pgtg_observe", "pgtg_get_counters",
-    "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_last_error", "pgtg_last_step_ms",
-    "pgtg_enable_timing",
+    "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_last_error", "pgtg_enable_timing",
+    "pgtg_timing_read",
 ]
 
 
@@ -92,6 +92,10 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} not built: run `python -m pgtg_amd.build` (HIP/gfx950); "
                            "there is no CPU fallback")
+    # torch ships its own libamdhip64/libhsa-runtime64 (same soname as /opt/rocm's).  Load it first
+    # so that this library binds to the process's single HIP runtime and shares torch's device
+    # memory and streams; loading ours first would start a second HSA runtime.
+    import torch  # noqa: F401
     L = C.CDLL(LIB_PATH)
     vp, u64, i32 = C.c_void_p, C.c_uint64, C.c_int32
     sig = {
@@ -114,7 +118,7 @@ def lib():
         "pgtg_window": ([vp], C.c_int),
         "pgtg_num_envs": ([vp], u64),
         "pgtg_last_error": ([vp], C.c_char_p),
-        "pgtg_last_step_ms": ([vp], C.c_float),
+        "pgtg_timing_read": ([vp, C.POINTER(C.c_double), C.POINTER(u64), i32], C.c_int),
         "pgtg_enable_timing": ([vp, i32], C.c_int),
     }
     for name, (args, res) in sig.items():

@@ -50,6 +50,7 @@ struct DevCfg {
   uint32_t fixed_sg;
   int32_t start_mode, goal_mode, sx, sy, sdir, gx, gy, gdir, min_distance;
   int32_t n_edges, keep;
+  uint64_t h0[4];  // full-grid exit masks (N, E, S, W) before removals
   uint8_t ea[kMaxEdges], eb[kMaxEdges], ed[kMaxEdges], erev[kMaxEdges];
   int32_t n_border, n_border_add;
   uint8_t bt[kMaxBorder], bd[kMaxBorder];
@@ -74,6 +75,19 @@ struct DevCfg {
   int32_t plan_stride;          // u16 per env in the global tile-plan array (multiple of 8)
   int32_t obs_bytes;            // n_channels * win * win
   int32_t mask_words;           // ceil(win*win/32)
+};
+
+// Lane-indexed constant tables, copied once per workgroup into LDS (sT in pgtg_env.hip): the
+// 81-bit tile masks, the graph-theory edge order, border candidates and per-path-length rewards.
+struct Tables {
+  uint32_t wall[16][3];     // kTileWall
+  uint32_t seg[4][3];       // kExitSeg
+  uint32_t obst[14][3];     // kObstMask
+  uint32_t spawner[16][3];  // kLaneSpawner
+  double ind[kMaxTiles + 1];  // sum_subgoals_reward / num_subgoals
+  uint8_t ea[kMaxEdges], eb[kMaxEdges], ed[kMaxEdges], erev[kMaxEdges];
+  uint8_t bt[kMaxBorder], bd[kMaxBorder];
+  uint32_t lanes[16][81];   // kLanes (copied only when traffic or lane/spawner channels need it)
 };
 
 // one PCG64 stream, SoA over envs

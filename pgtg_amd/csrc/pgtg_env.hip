@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <array>
+#include <cstddef>
 #include <string>
 #include <vector>
 
@@ -36,6 +37,25 @@ namespace hs {
 #include "pgtg_tables.h"
 #undef PGTG_TBL_QUAL
 }  // namespace hs
+
+__shared__ Tables sT;  // per-workgroup LDS copy of the lane-indexed tables
+
+// Diagnostic build only (-DPGTG_STAMPS): per-wave phase timestamps (s_memtime) into a debug buffer
+// that nothing else reads.  The product build compiles these to nothing.
+#ifdef PGTG_STAMPS
+__device__ unsigned long long g_stamps[1 << 20];
+#define STAMP(k)                                                                          \
+  do {                                                                                    \
+    if ((threadIdx.x & 63) == 0) {                                                        \
+      unsigned long long t_ = __builtin_amdgcn_s_memtime();                               \
+      g_stamps[((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16 + (k)) & ((1 << 20) - 1)] = t_; \
+    }                                                                                     \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // small device helpers
@@ -104,7 +124,7 @@ __device__ __forceinline__ uint32_t square_flags(const DevCfg& c, const Plan& pl
   uint32_t ex = plan_exits(p);
   int sq = lx * 9 + ly;
   uint32_t f = 0;
-  uint32_t wall = bit81(dv::kTileWall[ex], sq);
+  uint32_t wall = bit81(sT.wall[ex], sq);
   if (wall) f |= SQ_WALL;
   int d = seg_dir(lx, ly);
   if (d >= 0 && ((ex >> d) & 1u)) {
@@ -113,14 +133,14 @@ __device__ __forceinline__ uint32_t square_flags(const DevCfg& c, const Plan& pl
     if ((int)((v.sg >> 16) & 0xffu) == t && (int)(v.sg >> 24) == d) f |= SQ_FINAL;
   }
   uint32_t ot = plan_otype(p);
-  if (ot && !wall && bit81(dv::kObstMask[plan_omask(p)], sq)) f |= SQ_ICE << (ot - 1);
+  if (ot && !wall && bit81(sT.obst[plan_omask(p)], sq)) f |= SQ_ICE << (ot - 1);
   return f;
 }
 __device__ __forceinline__ uint32_t square_lanes(const DevCfg& c, const Plan& pl, int x, int y) {
   int tx = x / kTile, ty = y / kTile;
   int lx = x - tx * kTile, ly = y - ty * kTile;
   uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
-  return ex ? dv::kLanes[ex][lx * 9 + ly] : 0u;
+  return ex ? sT.lanes[ex][lx * 9 + ly] : 0u;
 }
 __device__ __forceinline__ bool square_spawner(const DevCfg& c, const Plan& pl, int x, int y) {
   int tx = x / kTile, ty = y / kTile;
@@ -128,8 +148,8 @@ __device__ __forceinline__ bool square_spawner(const DevCfg& c, const Plan& pl, 
   uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
   if (!ex) return false;
   int sq = lx * 9 + ly;
-  if (bit81(dv::kLaneSpawner[ex], sq)) return true;
-  uint32_t l = dv::kLanes[ex][sq];
+  if (bit81(sT.spawner[ex], sq)) return true;
+  uint32_t l = sT.lanes[ex][sq];
   return (tx == 0 && (l >> 31 & 1u)) || (tx == c.tw - 1 && (l >> 30 & 1u)) || (ty == 0 && (l >> 29 & 1u)) ||
          (ty == c.th - 1 && (l >> 28 & 1u));
 }
@@ -143,7 +163,7 @@ __device__ __forceinline__ int phase_color(const DevCfg& c, uint32_t ph) {
 // ------------------------------------------------------------------------------------------------
 // reset: seeding, procedural map, compilation, start square  (pgtg/environment.py:581-656)
 // ------------------------------------------------------------------------------------------------
-__device__ void rand_pos(const DevCfg& c, Pcg& r, int& x, int& y) {  // map_generator.py:602-626
+__device__ __forceinline__ void rand_pos(const DevCfg& c, Pcg& r, int& x, int& y) {  // map_generator.py:602-626
   switch (pcg_int(r, 4)) {
     case 0: x = (int)pcg_int(r, c.tw); y = 0; break;
     case 1: x = c.tw - 1; y = (int)pcg_int(r, c.th); break;
@@ -151,55 +171,126 @@ __device__ void rand_pos(const DevCfg& c, Pcg& r, int& x, int& y) {  // map_gene
     default: x = 0; y = (int)pcg_int(r, c.th); break;
   }
 }
-__device__ int rand_dir(const DevCfg& c, Pcg& r, int x, int y) {  // map_generator.py:574-599
-  int o[4], n = 0;
-  if (y == 0) o[n++] = 0;
-  if (x == c.tw - 1) o[n++] = 1;
-  if (y == c.th - 1) o[n++] = 2;
-  if (x == 0) o[n++] = 3;
-  int k = (int)pcg_int(r, (uint32_t)n);
-  return k == 0 ? o[0] : (k == 1 ? o[1] : (k == 2 ? o[2] : o[3]));
+__device__ __forceinline__ int rand_dir(const DevCfg& c, Pcg& r, int x, int y) {  // map_generator.py:574-599
+  // possible directions in the order north, east, south, west as a bitmask; pick the k-th set bit
+  uint32_t m = (y == 0 ? 1u : 0u) | (x == c.tw - 1 ? 2u : 0u) | (y == c.th - 1 ? 4u : 0u) | (x == 0 ? 8u : 0u);
+  int k = (int)pcg_int(r, (uint32_t)__popc(m));
+  for (int j = 0; j < k; j++) m &= m - 1u;
+  return __ffs((int)m) - 1;
 }
 
-template <int NW>
-__device__ __forceinline__ int select_kth(const uint64_t (&m)[NW], int k) {
-  int base = 0, res = -1;
-#pragma unroll
-  for (int w = 0; w < NW; w++) {
-    int cnt = __popcll(m[w]);
-    if (res < 0) {
-      if (k < cnt) {
-        uint64_t x = m[w];
-        for (int i = 0; i < k; i++) x &= x - 1ull;
-        res = base + __ffsll((long long)x) - 1;
-      } else {
-        k -= cnt;
-      }
-    }
-    base += 64;
+// 256-bit set kept in four named registers (no private-array indexing -> no scratch)
+struct Bits256 {
+  uint64_t w0, w1, w2, w3;
+  __device__ __forceinline__ void init(int n) {
+    w0 = n >= 64 ? ~0ull : (n <= 0 ? 0ull : ((1ull << n) - 1ull));
+    w1 = n >= 128 ? ~0ull : (n <= 64 ? 0ull : ((1ull << (n - 64)) - 1ull));
+    w2 = n >= 192 ? ~0ull : (n <= 128 ? 0ull : ((1ull << (n - 128)) - 1ull));
+    w3 = n >= 256 ? ~0ull : (n <= 192 ? 0ull : ((1ull << (n - 192)) - 1ull));
   }
-  return res;
-}
-template <int NW>
-__device__ __forceinline__ void clear_bit(uint64_t (&m)[NW], int i) {
-#pragma unroll
-  for (int w = 0; w < NW; w++)
-    if (w == (i >> 6)) m[w] &= ~(1ull << (i & 63));
+  __device__ __forceinline__ void clear(int i) {
+    uint64_t m = ~(1ull << (i & 63));
+    int q = i >> 6;
+    w0 &= q == 0 ? m : ~0ull;
+    w1 &= q == 1 ? m : ~0ull;
+    w2 &= q == 2 ? m : ~0ull;
+    w3 &= q == 3 ? m : ~0ull;
+  }
+  // index of the k-th (0-based) set bit
+  __device__ __forceinline__ int select(int k) const {
+    int c0 = __popcll(w0), c1 = __popcll(w1), c2 = __popcll(w2);
+    uint64_t x;
+    int base;
+    if (k < c0) { x = w0; base = 0; }
+    else if (k < c0 + c1) { x = w1; base = 64; k -= c0; }
+    else if (k < c0 + c1 + c2) { x = w2; base = 128; k -= c0 + c1; }
+    else { x = w3; base = 192; k -= c0 + c1 + c2; }
+    // k-th set bit of x by halving with popcounts
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    int cl = __popc(lo);
+    uint32_t y = k < cl ? lo : hi;
+    if (k >= cl) { base += 32; k -= cl; }
+    int c16 = __popc(y & 0xffffu);
+    if (k >= c16) { y >>= 16; base += 16; k -= c16; }
+    int c8 = __popc(y & 0xffu);
+    if (k >= c8) { y >>= 8; base += 8; k -= c8; }
+    for (int j = 0; j < k; j++) y &= y - 1u;
+    return base + __ffs((int)y) - 1;
+  }
+};
+
+// One BFS step on the symmetric tile graph given by the four exit masks.
+template <typename M>
+__device__ __forceinline__ M expand(M R, M hN, M hE, M hS, M hW, int w) {
+  return R | ((R & hN) >> w) | ((R & hS) << w) | ((R & hE) << 1) | ((R & hW) >> 1);
 }
 
-// start tile reaches goal tile in the symmetric tile graph given by the four exit masks
-__device__ __forceinline__ bool connected(uint64_t hN, uint64_t hE, uint64_t hS, uint64_t hW, int w, int s, int g) {
-  uint64_t R = 1ull << s, goal = 1ull << g;
+// After deleting edge a-b from a graph in which start s and goal g were connected: are they still?
+// Bidirectional flood from a and b: the fronts meet (a-b still connected -> yes), or one side's
+// component is exhausted first, in which case s-g broke iff exactly one of s, g lies in it.
+template <typename M>
+__device__ __forceinline__ bool still_connected(M hN, M hE, M hS, M hW, int w, int a, int b, int s, int g) {
+  M Ra = (M)1 << a, Rb = (M)1 << b;
   for (;;) {
-    uint64_t N = R | ((R & hN) >> w) | ((R & hS) << w) | ((R & hE) << 1) | ((R & hW) >> 1);
-    if (N & goal) return true;
-    if (N == R) return false;
-    R = N;
+    M Na = expand<M>(Ra, hN, hE, hS, hW, w);
+    M Nb = expand<M>(Rb, hN, hE, hS, hW, w);
+    if (Na & Nb) return true;
+    if (Na == Ra) return ((Ra >> s) & 1) == ((Ra >> g) & 1);
+    if (Nb == Rb) return ((Rb >> s) & 1) == ((Rb >> g) & 1);
+    Ra = Na;
+    Rb = Nb;
+  }
+}
+
+// generate_map_graph's edge-removal loop (map_generator.py:218-264) on exit masks of type M
+// (uint32_t when the map has <= 32 tiles).  removable_edges keeps graph-theory's nested-dict order
+// (host table ea/eb/ed/erev); an edge pair stays removed iff start->end stays connected, which is
+// exactly the outcome of the reference's BFS-path test + re-add.  A removed edge whose two tiles
+// still share an intact 4-cycle cannot disconnect anything; otherwise still_connected decides.
+template <typename M>
+__device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, int gl_t, M& hN, M& hE, M& hS, M& hW) {
+  const int w = c.tw;
+  Bits256 L;
+  L.init(c.n_edges);
+  int nrem = c.n_edges, count = c.n_edges;
+  while (count > c.keep && nrem > 0) {
+    int k = (int)pcg_int(r, (uint32_t)nrem);
+    int e = L.select(k);
+    int e2 = sT.erev[e];
+    L.clear(e);
+    L.clear(e2);
+    nrem -= 2;
+    int a = sT.ea[e], b = sT.eb[e], d = sT.ed[e];
+    if (d == 0 || d == 3) {  // orient: a = north/west tile, d in {E (1), S (2)}
+      int t = a; a = b; b = t;
+      d = d == 0 ? 2 : 1;
+    }
+    const M ma = (M)1 << a, mb = (M)1 << b;
+    const M sN = hN, sE = hE, sS = hS, sW = hW;
+    bool cyc;
+    if (d == 1) {  // horizontal a | b
+      hE &= ~ma;
+      hW &= ~mb;
+      bool up = (hN & ma) && (hN & mb) && (hE & (ma >> w));
+      bool dn = (hS & ma) && (hS & mb) && (hE & (ma << w));
+      cyc = up || dn;
+    } else {       // vertical a over b
+      hS &= ~ma;
+      hN &= ~mb;
+      bool lf = (hW & ma) && (hW & mb) && (hS & (ma >> 1));
+      bool rt = (hE & ma) && (hE & mb) && (hS & (ma << 1));
+      cyc = lf || rt;
+    }
+    count -= 2;
+    if (!cyc && !still_connected<M>(hN, hE, hS, hW, w, a, b, st_t, gl_t)) {
+      hN = sN; hE = sE; hS = sS; hW = sW;
+      count += 2;
+    }
   }
 }
 
 // generate_map (map_generator.py:43-189) -> tile plan (exits + obstacles) in LDS, start/goal
-__device__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* plan, int& st_t, int& st_d, int& gl_t, int& gl_d) {
+__device__ __forceinline__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* plan, int& st_t, int& st_d, int& gl_t, int& gl_d) {
   const int w = c.tw;
   // chose_random_start_and_goal_position_and_direction (map_generator.py:475-571)
   int s0, s1, s2 = c.sdir, g0, g1, g2 = c.gdir;
@@ -242,49 +333,20 @@ __device__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* plan, int& st_t,
   st_d = s2;
   gl_t = g1 * w + g0;
   gl_d = g2;
+  STAMP(13);
 
-  // generate_map_graph (map_generator.py:192-266).  removable_edges keeps graph-theory's nested
-  // dict order (host table ea/eb); an edge pair stays removed iff start->end stays connected,
-  // which is exactly the outcome of the reference's BFS-path test + re-add.
-  uint64_t hN = 0, hE = 0, hS = 0, hW = 0;
-  uint64_t L[4] = {0, 0, 0, 0};
-  for (int e = 0; e < c.n_edges; e++) {
-    int a = c.ea[e];
-    switch (c.ed[e]) {
-      case 0: hN |= 1ull << a; break;
-      case 1: hE |= 1ull << a; break;
-      case 2: hS |= 1ull << a; break;
-      default: hW |= 1ull << a; break;
-    }
+  // generate_map_graph (map_generator.py:192-266): full grid (host masks c.h0), then removals
+  uint64_t hN, hE, hS, hW;
+  STAMP(14);
+  if (c.nt <= 32) {
+    uint32_t n = (uint32_t)c.h0[0], e = (uint32_t)c.h0[1], so = (uint32_t)c.h0[2], we = (uint32_t)c.h0[3];
+    remove_edges<uint32_t>(c, r, st_t, gl_t, n, e, so, we);
+    hN = n; hE = e; hS = so; hW = we;
+  } else {
+    hN = c.h0[0]; hE = c.h0[1]; hS = c.h0[2]; hW = c.h0[3];
+    remove_edges<uint64_t>(c, r, st_t, gl_t, hN, hE, hS, hW);
   }
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    int lo = q * 64, n = c.n_edges - lo;
-    L[q] = n >= 64 ? ~0ull : (n <= 0 ? 0ull : ((1ull << n) - 1ull));
-  }
-  int nrem = c.n_edges, count = c.n_edges;
-  while (count > c.keep && nrem > 0) {
-    int k = (int)pcg_int(r, (uint32_t)nrem);
-    int e = select_kth<4>(L, k);
-    int e2 = c.erev[e];
-    clear_bit<4>(L, e);
-    clear_bit<4>(L, e2);
-    nrem -= 2;
-    int a = c.ea[e], b = c.eb[e], d = c.ed[e];
-    uint64_t ma = 1ull << a, mb = 1ull << b;
-    uint64_t sN = hN, sE = hE, sS = hS, sW = hW;
-    switch (d) {  // remove a->b and b->a
-      case 0: hN &= ~ma; hS &= ~mb; break;
-      case 1: hE &= ~ma; hW &= ~mb; break;
-      case 2: hS &= ~ma; hN &= ~mb; break;
-      default: hW &= ~ma; hE &= ~mb; break;
-    }
-    count -= 2;
-    if (!connected(hN, hE, hS, hW, w, st_t, gl_t)) {
-      hN = sN; hE = sE; hS = sS; hW = sW;
-      count += 2;
-    }
-  }
+  STAMP(15);
   // map_graph_to_tile_map_object (map_generator.py:269-334): exits straight into the LDS plan
   for (int t = 0; t < c.nt; t++)
     plan[t] = (uint16_t)((uint32_t)((hN >> t) & 1ull) | (uint32_t)((hE >> t) & 1ull) << 1 |
@@ -292,18 +354,14 @@ __device__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* plan, int& st_t,
   plan[st_t] |= (uint16_t)(1u << st_d);
   plan[gl_t] |= (uint16_t)(1u << gl_d);
   // add_connections_to_borders (map_generator.py:337-371), candidate list from the host
-  uint64_t B[3] = {0, 0, 0};
-#pragma unroll
-  for (int q = 0; q < 3; q++) {
-    int n = c.n_border - q * 64;
-    B[q] = n >= 64 ? ~0ull : (n <= 0 ? 0ull : ((1ull << n) - 1ull));
-  }
+  Bits256 B;
+  B.init(c.n_border);
   int nb = c.n_border;
   for (int k = 0; k < c.n_border_add; k++) {
-    int j = select_kth<3>(B, (int)pcg_int(r, (uint32_t)nb));
-    clear_bit<3>(B, j);
+    int j = B.select((int)pcg_int(r, (uint32_t)nb));
+    B.clear(j);
     nb--;
-    plan[c.bt[j]] |= (uint16_t)(1u << c.bd[j]);
+    plan[sT.bt[j]] |= (uint16_t)(1u << sT.bd[j]);
   }
   // add_obstacles_to_map (map_generator.py:374-472)
   if (c.obstacle_probability > 0.0) {
@@ -316,22 +374,13 @@ __device__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* plan, int& st_t,
         if (ot != 3) {
           om = pcg_int(r, 8);
         } else {
+          // traffic-light masks in list order: north, east, south, west, north_and_south,
+          // east_and_west (the last two only at >= 3 exits); option j <-> mask id 8 + j
           int n = __popc(e);
-          uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0, o4 = 0, o5 = 0;
-          int m = 0;
-          auto push = [&](uint32_t val) {
-            if (m == 0) o0 = val; else if (m == 1) o1 = val; else if (m == 2) o2 = val;
-            else if (m == 3) o3 = val; else if (m == 4) o4 = val; else o5 = val;
-            m++;
-          };
-          if (e & 1u) push(8);
-          if (e & 2u) push(9);
-          if (e & 4u) push(10);
-          if (e & 8u) push(11);
-          if ((e & 1u) && (e & 4u) && n >= 3) push(12);
-          if ((e & 2u) && (e & 8u) && n >= 3) push(13);
-          int k = (int)pcg_int(r, (uint32_t)m);
-          om = k == 0 ? o0 : k == 1 ? o1 : k == 2 ? o2 : k == 3 ? o3 : k == 4 ? o4 : o5;
+          uint32_t opt = (e & 15u) | (((e & 5u) == 5u && n >= 3) ? 16u : 0u) | (((e & 10u) == 10u && n >= 3) ? 32u : 0u);
+          int k = (int)pcg_int(r, (uint32_t)__popc(opt));
+          for (int j = 0; j < k; j++) opt &= opt - 1u;
+          om = (uint32_t)(8 + __ffs((int)opt) - 1);
         }
         plan[t] = (uint16_t)(e | (uint32_t)(ot + 1) << 4 | om << 7);
       }
@@ -341,7 +390,7 @@ __device__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* plan, int& st_t,
 
 // parse_map_object's shortest path (graph-theory Dijkstra == FIFO BFS, neighbours N,E,S,W)
 // -> subgoal directions in the plan; returns the path length (num_subgoals) or 0.
-__device__ int compile_path(const DevCfg& c, uint16_t* plan, uint8_t* q, uint8_t* par, int s, int g) {
+__device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, uint8_t* q, uint8_t* par, int s, int g) {
   const int w = c.tw, h = c.th;
   uint64_t seen = 1ull << s;
   int qh = 0, qt = 0;
@@ -380,8 +429,9 @@ __device__ int compile_path(const DevCfg& c, uint16_t* plan, uint8_t* q, uint8_t
 }
 
 // The full per-env reset.  `key` = spawn counter (5 children per episode).  Returns 0 or -code.
-__device__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, uint16_t* plan, uint8_t* q,
+__device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, uint16_t* plan, uint8_t* q,
                          uint8_t* par) {
+  STAMP(8);
   uint64_t seed = S.seed[i];
   SeedPool sp = ss_pool(seed);
   uint32_t k = v.spawn;
@@ -391,6 +441,7 @@ __device__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView
   if (c.need_broken) stream_store_all(S.broken, i, ss_child(sp, k + 3u));
   if (c.need_sand) stream_store_all(S.sand, i, ss_child(sp, k + 4u));
   v.spawn = k + 5u;
+  STAMP(9);
   int st_t, st_d, gl_t, gl_d;
   if (c.fixed_map) {
     for (int t = 0; t < c.nt; t++) plan[t] = c.fixed_plan[t];
@@ -402,7 +453,9 @@ __device__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView
     generate_map(c, map_rng, plan, st_t, st_d, gl_t, gl_d);
   }
   v.sg = (uint32_t)st_t | (uint32_t)st_d << 8 | (uint32_t)gl_t << 16 | (uint32_t)gl_d << 24;
+  STAMP(10);
   int len = compile_path(c, plan, q, par, st_t, gl_t);
+  STAMP(11);
   v.used = 0;
   v.path_len = (uint32_t)len;
   v.flags = 0;
@@ -424,6 +477,7 @@ __device__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView
   }
   v.px = tx * kTile + lx;
   v.py = ty * kTile + ly;
+  STAMP(12);
   if (S.visited) {
     uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
     for (int q2 = 0; q2 < c.vis_words; q2++) vis[q2] = 0;
@@ -464,7 +518,7 @@ struct ObsInfo {
 };
 
 // nearest subgoal / final goal square from (x, y): min Manhattan, x-major first (environment.py:1471-1480)
-__device__ bool nearest_goal_square(const DevCfg& c, const Plan& pl, const EnvView& v, int x, int y, int& bx, int& by) {
+__device__ __forceinline__ bool nearest_goal_square(const DevCfg& c, const Plan& pl, const EnvView& v, int x, int y, int& bx, int& by) {
   int best = 0x7fffffff;
   bool found = false;
   int gl_t = (int)((v.sg >> 16) & 0xffu), gl_d = (int)(v.sg >> 24);
@@ -498,12 +552,14 @@ __device__ bool nearest_goal_square(const DevCfg& c, const Plan& pl, const EnvVi
   return found;
 }
 
-__device__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v, uint32_t* masks,
-                          ObsInfo& oi) {
+// Observation of one env into its LDS segments: channel ci occupies words seg[ci*MW .. +MW) with
+// bit b = window square b (row-major over x, then y), unused high bits zero.  Plain stores only.
+__device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
+                                          uint32_t* seg, ObsInfo& oi) {
   int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
   int tx = pix / kTile, ty = piy / kTile;
   int color = phase_color(c, v.phase);
-  const int MW = c.mask_words;
+  const int WW = c.win * c.win, MW = c.mask_words;
   if (!c.sliding) {
     oi.x0 = tx * kTile;
     oi.y0 = ty * kTile;
@@ -527,15 +583,15 @@ __device__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, co
     uint32_t ot = plan_otype(p);
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-      W3[k] = dv::kTileWall[ex][k];
-      if (sd >= 0 && ((ex >> sd) & 1u)) (used ? US : SG)[k] = dv::kExitSeg[sd][k];
-      if (t == gl_t && ((ex >> gl_d) & 1u)) FI[k] = dv::kExitSeg[gl_d][k];
-      if (t == st_t && ((ex >> st_d) & 1u)) ST[k] = dv::kExitSeg[st_d][k];
-      if (ot) OB[k] = dv::kObstMask[plan_omask(p)][k] & ~W3[k];
+      W3[k] = sT.wall[ex][k];
+      if (sd >= 0 && ((ex >> sd) & 1u)) (used ? US : SG)[k] = sT.seg[sd][k];
+      if (t == gl_t && ((ex >> gl_d) & 1u)) FI[k] = sT.seg[gl_d][k];
+      if (t == st_t && ((ex >> st_d) & 1u)) ST[k] = sT.seg[st_d][k];
+      if (ot) OB[k] = sT.obst[plan_omask(p)][k] & ~W3[k];
     }
     for (int ci = 0; ci < c.n_channels; ci++) {
       int code = c.channels[ci];
-      uint32_t* m = masks + ci * MW;
+      uint32_t out3[3];
 #pragma unroll
       for (int k = 0; k < 3; k++) {
         uint32_t val;
@@ -554,31 +610,38 @@ __device__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, co
           case PGTG_CH_SAND: val = ot == 3 ? OB[k] : 0u; break;
           default: val = 0u; break;  // PGTG_CH_ZERO, PGTG_CH_TRAFFIC (filled by the traffic pass)
         }
-        m[k] = val;
+        out3[k] = val;
       }
+      seg[ci * 3 + 0] = out3[0];
+      seg[ci * 3 + 1] = out3[1];
+      seg[ci * 3 + 2] = out3[2] & 0x1ffffu;  // 81 = 32 + 32 + 17 bits
     }
   } else {
     const int win = c.win;
-    for (int ci = 0; ci < c.n_channels; ci++)
-      for (int k = 0; k < MW; k++) masks[ci * MW + k] = 0u;
-    for (int i = 0; i < win; i++)
-      for (int j = 0; j < win; j++) {
-        int x = oi.x0 + i, y = oi.y0 + j;
-        uint32_t f, lanes = 0;
-        bool sp = false;
-        if (inside(c, x, y)) {
-          f = square_flags(c, pl, v, x, y);
-          if (c.generic_channels) {
-            lanes = square_lanes(c, pl, x, y);
-            sp = square_spawner(c, pl, x, y);
+    for (int ci = 0; ci < c.n_channels; ci++) {
+      int code = c.channels[ci];
+      for (int w0 = 0; w0 < WW; w0 += 32) {
+        uint32_t acc = 0;
+        if (code != PGTG_CH_ZERO && code != PGTG_CH_TRAFFIC) {
+          int nb = min(32, WW - w0);
+          for (int b = 0; b < nb; b++) {
+            int bb = w0 + b, i = bb / win, j = bb - i * win;
+            int x = oi.x0 + i, y = oi.y0 + j;
+            uint32_t f, lanes = 0;
+            bool sp = false;
+            if (inside(c, x, y)) {
+              f = square_flags(c, pl, v, x, y);
+              if (code == PGTG_CH_SPAWNER) sp = square_spawner(c, pl, x, y);
+              if (code >= PGTG_CH_LANE0) lanes = square_lanes(c, pl, x, y);
+            } else {
+              f = c.sliding ? SQ_WALL : 0u;  // get_map_cutout fill {"wall"} for sliding windows
+            }
+            acc |= chan_bit(code, f, lanes, sp, color) << b;
           }
-        } else {
-          f = c.sliding ? SQ_WALL : 0u;  // get_map_cutout fill {"wall"} for sliding windows
         }
-        int b = i * win + j;
-        for (int ci = 0; ci < c.n_channels; ci++)
-          masks[ci * MW + (b >> 5)] |= chan_bit(c.channels[ci], f, lanes, sp, color) << (b & 31);
+        seg[ci * MW + (w0 >> 5)] = acc;
       }
+    }
   }
   oi.nsd = -1;
   if (c.next_subgoal) {
@@ -598,21 +661,22 @@ __device__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, co
 // ------------------------------------------------------------------------------------------------
 // step (pgtg/environment.py:1092-1281) for one lane; returns 0 or -code
 // ------------------------------------------------------------------------------------------------
-constexpr int ACCX[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
-constexpr int ACCY[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1};
+// ACTIONS_TO_ACCELERATION (pgtg/constants.py:6-16): action a -> (a/3 - 1, a%3 - 1)
+__device__ __forceinline__ int acc_x(int a) { return a / 3 - 1; }
+__device__ __forceinline__ int acc_y(int a) { return a % 3 - 1; }
 
 struct StepResult {
   double reward, cost;
 };
 
-__device__ int env_step(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, const Plan& pl, int action,
+__device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, const Plan& pl, int action,
                         StepResult& res) {
   res.reward = 0.0;
   res.cost = 0.0;
   if (v.flags & (kFlagTerminated | kFlagTruncated)) return PGTG_E_DONE;
   if ((unsigned)action > 8u) return PGTG_E_INVALID;
   v.phase = (v.phase + 1u) % (uint32_t)c.phase_total;
-  const int ax = ACCX[action], ay = ACCY[action];
+  const int ax = acc_x(action), ay = acc_y(action);
   double reward = 0.0, perf = 0.0, cost = 0.0;
   int cx = v.px, cy = v.py;
   v.vx += ax;
@@ -649,13 +713,13 @@ __device__ int env_step(const DevCfg& c, const DevState& S, uint64_t i, EnvView&
       break;
     }
     if (f & SQ_FINAL) {
-      double add = c.ind_reward[v.path_len] + c.final_goal_bonus;
+      double add = sT.ind[v.path_len] + c.final_goal_bonus;
       if (c.separate_cost) perf += add; else reward += add;
       v.flags |= kFlagTerminated;
       break;
     }
     if (f & SQ_SUBGOAL) {
-      if (c.separate_cost) perf += c.ind_reward[v.path_len]; else reward += c.ind_reward[v.path_len];
+      if (c.separate_cost) perf += sT.ind[v.path_len]; else reward += sT.ind[v.path_len];
       // set_subgoals_to_used: the flood fill covers exactly this tile's subgoal segment
       v.used |= 1ull << ((cy / kTile) * c.tw + cx / kTile);
     }
@@ -687,8 +751,8 @@ __device__ int env_step(const DevCfg& c, const DevState& S, uint64_t i, EnvView&
       used_ice = true;
       if (pcg_double(ice) < c.ice_p) {
         int a = (int)pcg_int(ice, 9);
-        pxp = ACCX[a];
-        pyp = ACCY[a];
+        pxp = acc_x(a);
+        pyp = acc_y(a);
       }
     }
     if (f & SQ_BROKEN) {
@@ -736,68 +800,60 @@ __device__ int env_step(const DevCfg& c, const DevState& S, uint64_t i, EnvView&
 }
 
 // ------------------------------------------------------------------------------------------------
-// cooperative observation writer: the workgroup's contiguous [nb][obs_bytes] slice, 16-B stores
+// cooperative observation writer: the output slice [cnt][obs_bytes] of `cnt` consecutive envs is
+// the LDS segment image expanded bit -> byte, written with 16-byte stores.  Bytes outside the slice
+// are never touched (neighbouring slices belong to other workgroups).  With sel != null a chunk is
+// written only if one of its envs has sel == 1: final observations of the other envs are
+// unspecified (gymnasium's info["final_observation"] is valid where "_final_observation" is set).
 // ------------------------------------------------------------------------------------------------
-__device__ void write_obs_block(const DevCfg& c, uint8_t* __restrict__ dst, uint64_t env0, int nb,
-                                const uint32_t* __restrict__ masks, int mstride, const uint8_t* __restrict__ sel) {
-  const int OB = c.obs_bytes, MW = c.mask_words, WW = c.win * c.win;
-  uint8_t* base = dst + env0 * (uint64_t)OB;
-  const uint64_t total = (uint64_t)nb * OB;
-  const uintptr_t a0 = (uintptr_t)base, a1 = a0 + total;
+__device__ __forceinline__ uint32_t expand4(uint32_t x) { return ((x & 15u) * 0x00204081u) & 0x01010101u; }
+// floor(x / d) for x < 2^24 via an f32 reciprocal and one correction step each way
+__device__ __forceinline__ uint32_t udiv_f(uint32_t x, uint32_t d, float inv) {
+  uint32_t q = (uint32_t)((float)x * inv);
+  if (q * d > x) q--;
+  if ((q + 1) * d <= x) q++;
+  return q;
+}
+
+__device__ __forceinline__ void write_obs(uint8_t* __restrict__ dst, uint32_t cnt, uint32_t WW, uint32_t MW,
+                                          uint32_t C, const uint32_t* st, const uint8_t* sel) {
+  const uint32_t OB = C * WW, total = cnt * OB;
+  const uintptr_t a0 = (uintptr_t)dst;
   const uintptr_t c0 = a0 & ~(uintptr_t)15;
-  const uint64_t nchunks = (a1 - c0 + 15) >> 4;
-  for (uint64_t ch = threadIdx.x; ch < nchunks; ch += blockDim.x) {
-    uintptr_t ca = c0 + (ch << 4);
-    uint8_t bytes[16];
-    bool full = true, any = false;
-    int64_t r = (int64_t)(ca - a0);
-    // decompose the first byte's offset once, then walk
-    int e = 0, rem = 0;
-    if (r >= 0) {
-      e = (int)(r / OB);
-      rem = (int)(r - (int64_t)e * OB);
+  const uint32_t nchunks = (uint32_t)((a0 + total - c0 + 15) >> 4);
+  const float invWW = 1.0f / (float)WW, invOB = 1.0f / (float)OB;
+  for (uint32_t ch = threadIdx.x; ch < nchunks; ch += blockDim.x) {
+    const int r = (int)((intptr_t)(c0 + ((uintptr_t)ch << 4)) - (intptr_t)a0);  // > -16
+    const uint32_t lo = r < 0 ? 0u : (uint32_t)r;
+    const uint32_t hi = min((uint32_t)(r + 15), total - 1u);
+    if (sel) {
+      const uint32_t e0 = udiv_f(lo, OB, invOB), e1 = udiv_f(hi, OB, invOB);
+      bool any = false;
+      for (uint32_t e = e0; e <= e1; e++) any = any || sel[e] == 1;
+      if (!any) continue;
     }
-    int ci = rem / WW, sq = rem - ci * WW;
-#pragma unroll
-    for (int b = 0; b < 16; b++) {
-      int64_t rb = r + b;
-      uint8_t val = 0;
-      bool in = rb >= 0 && (uint64_t)rb < total && (sel == nullptr || sel[rb >= 0 ? e : 0]);
-      if (in) {
-        const uint32_t* m = masks + e * mstride + ci * MW;
-        val = (uint8_t)((m[sq >> 5] >> (sq & 31)) & 1u);
-        any = true;
-      } else {
-        full = false;
-      }
-      bytes[b] = val;
-      if (rb >= 0) {  // advance (e, ci, sq)
-        if (++sq == WW) {
-          sq = 0;
-          if (++ci == c.n_channels) {
-            ci = 0;
-            ++e;
-          }
-        }
-      }
+    // gather bits lo..hi from the segment image
+    uint32_t g = udiv_f(lo, WW, invWW), sq = lo - g * WW;
+    uint32_t bits = 0;
+    int got = (int)lo - r;  // bit index inside the chunk of byte `lo`
+    const int need = (int)hi - r + 1;
+    while (got < need) {
+      uint32_t take = min((uint32_t)(need - got), WW - sq);
+      uint32_t wi = g * MW + (sq >> 5), sh = sq & 31u;
+      uint64_t two = (uint64_t)st[wi] | ((uint64_t)st[wi + 1] << 32);
+      uint32_t part = (uint32_t)(two >> sh) & ((1u << take) - 1u);
+      bits |= part << got;
+      got += (int)take;
+      g++;
+      sq = 0;
     }
-    if (full) {
-      uint4 w;
-      w.x = bytes[0] | bytes[1] << 8 | bytes[2] << 16 | (uint32_t)bytes[3] << 24;
-      w.y = bytes[4] | bytes[5] << 8 | bytes[6] << 16 | (uint32_t)bytes[7] << 24;
-      w.z = bytes[8] | bytes[9] << 8 | bytes[10] << 16 | (uint32_t)bytes[11] << 24;
-      w.w = bytes[12] | bytes[13] << 8 | bytes[14] << 16 | (uint32_t)bytes[15] << 24;
-      *reinterpret_cast<uint4*>(ca) = w;
-    } else if (any) {
-      int64_t rr = r;
-      int ee = e;
-      (void)ee;
+    uint8_t* cp = dst + r;  // 16-byte aligned
+    if (r >= 0 && (uint32_t)r + 16u <= total) {
+      *reinterpret_cast<uint4*>(cp) = make_uint4(expand4(bits), expand4(bits >> 4), expand4(bits >> 8), expand4(bits >> 12));
+    } else {
       for (int b = 0; b < 16; b++) {
-        int64_t rb = rr + b;
-        if (rb < 0 || (uint64_t)rb >= total) continue;
-        int eb = (int)(rb / OB);
-        if (sel != nullptr && !sel[eb]) continue;
-        reinterpret_cast<uint8_t*>(ca)[b] = bytes[b];
+        int rb = r + b;
+        if (rb >= 0 && (uint32_t)rb < total) cp[b] = (uint8_t)((bits >> b) & 1u);
       }
     }
   }
@@ -807,22 +863,30 @@ __device__ void write_obs_block(const DevCfg& c, uint8_t* __restrict__ dst, uint
 // kernels
 // ------------------------------------------------------------------------------------------------
 struct Lds {
+  int envs;            // envs per workgroup (<= kBlock); lanes >= envs only help with the writes
   int plan_stride_dw;  // per-lane plan words (odd)
   int scratch_dw;      // per-lane BFS scratch words (odd)
-  int mask_stride;     // per-lane obs mask words (odd)
+  int seg_words;       // per-env observation words (n_channels * mask_words)
+  int sub_envs;        // envs per observation sub-batch (== envs when they all fit)
+  int stream_words;    // observation image words (+2 pad)
 };
 
 __host__ __device__ inline int odd_up(int x) { return x | 1; }
 
-__host__ inline Lds lds_layout(const DevCfg& c) {
+__host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   Lds l;
+  l.envs = envs;
   l.plan_stride_dw = odd_up((c.nt + 1) / 2);
   l.scratch_dw = odd_up((2 * c.nt + 3) / 4);
-  l.mask_stride = odd_up(c.n_channels * c.mask_words);
+  l.seg_words = c.n_channels * c.mask_words;
+  const int budget_words = 12 * 1024;  // 48 KiB observation image
+  int sub = l.seg_words > 0 ? (budget_words - 2) / l.seg_words : envs;
+  l.sub_envs = sub > envs ? envs : (sub < 1 ? 1 : sub);
+  l.stream_words = l.sub_envs * l.seg_words + 2;
   return l;
 }
 __host__ inline size_t lds_bytes(const Lds& l) {
-  return (size_t)kBlock * 4 * (l.plan_stride_dw + l.scratch_dw + l.mask_stride) + kBlock * 2;
+  return (size_t)4 * ((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw) + l.stream_words) + kBlock;
 }
 
 enum { MODE_STEP = 0, MODE_RESET_SEEDED = 1, MODE_RESET_UNSEEDED = 2, MODE_OBSERVE = 3 };
@@ -840,32 +904,58 @@ __device__ __forceinline__ void write_small_outputs(const DevCfg& c, const PgtgO
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, DevState S,
-                                                 const uint8_t* __restrict__ actions, const uint8_t* __restrict__ mask,
-                                                 PgtgOutputs out, int mode, Lds L) {
+// Observation pass over sub-batches: build the envs with want != 0 (small outputs as final or not)
+// into the segment image, then write the image slice to dst (selection sel).
+__device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
+                                         const PgtgOutputs& o, uint8_t* dst, uint64_t env0, int nb, bool want,
+                                         bool final, const uint8_t* sel, uint32_t* st, const Lds& L) {
+  const int tid = threadIdx.x;
+  for (int sb = 0; sb < nb; sb += L.sub_envs) {
+    const int cnt = min(L.sub_envs, nb - sb);
+    if (want && tid >= sb && tid < sb + cnt) {
+      ObsInfo oi;
+      build_obs(c, S, pl, v, st + (tid - sb) * L.seg_words, oi);
+      write_small_outputs(c, o, env0 + tid, v, oi, final);
+    }
+    __syncthreads();
+    if (dst)
+      write_obs(dst + (env0 + sb) * (uint64_t)c.obs_bytes, (uint32_t)cnt, (uint32_t)(c.win * c.win),
+                (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel ? sel + sb : nullptr);
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
+                                                 DevState S, const uint8_t* __restrict__ actions,
+                                                 const uint8_t* __restrict__ mask, PgtgOutputs out, int mode, Lds L) {
   extern __shared__ uint32_t lds[];
   const DevCfg& c = *cfg;
   const int tid = threadIdx.x;
-  const uint64_t env0 = (uint64_t)blockIdx.x * kBlock;
-  const int nb = (int)min((uint64_t)kBlock, S.n - env0);
+  STAMP(0);
+  // stage the lane-indexed tables (kLanes only when a pass needs it)
+  {
+    const int words = (int)((offsetof(Tables, lanes) + (c.generic_channels || c.need_car ? sizeof(sT.lanes) : 0)) / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
+    uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
+    for (int k = tid; k < words; k += blockDim.x) dstt[k] = src[k];
+  }
+  const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
+  const int nb = (int)min((uint64_t)L.envs, S.n - env0);
   const uint64_t i = env0 + tid;
   const bool live = tid < nb;
-  uint32_t* plan_w = lds + tid * L.plan_stride_dw;
-  uint32_t* scr_w = lds + kBlock * L.plan_stride_dw + tid * L.scratch_dw;
-  uint32_t* masks_all = lds + kBlock * (L.plan_stride_dw + L.scratch_dw);
-  uint32_t* masks = masks_all + tid * L.mask_stride;
-  uint8_t* sel = reinterpret_cast<uint8_t*>(masks_all + kBlock * L.mask_stride);  // [kBlock] terminal flags
+  const int lane_slot = tid < L.envs ? tid : 0;
+  uint32_t* plan_w = lds + lane_slot * L.plan_stride_dw;
+  uint32_t* scr_w = lds + L.envs * L.plan_stride_dw + lane_slot * L.scratch_dw;
+  uint32_t* st = lds + L.envs * (L.plan_stride_dw + L.scratch_dw);
+  uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
   Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
   uint8_t* q = reinterpret_cast<uint8_t*>(scr_w);
   uint8_t* par = q + c.nt;
 
   EnvView v{};
-  bool done = false;
   int err = 0;
-  StepResult res{0.0, 0.0};
   if (live) {
     v = rec_load(S.rec, i);
-    // stage the tile plan (16-B vector loads) into this lane's LDS slot
     const uint4* src = reinterpret_cast<const uint4*>(S.plan + i * (uint64_t)c.plan_stride);
     for (int k = 0; k < c.plan_stride / 8; k++) {
       uint4 w4 = src[k];
@@ -874,63 +964,81 @@ __global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, 
       for (int j = 0; j < 4; j++)
         if (k * 4 + j < L.plan_stride_dw) plan_w[k * 4 + j] = wv[j];
     }
-    bool do_reset = false;
+  }
+  __syncthreads();  // sT ready
+  STAMP(1);
+  uint8_t my_sel = 0;
+  if (live) {
     if (mode == MODE_STEP) {
+      StepResult res{0.0, 0.0};
       err = env_step(c, S, i, v, pl, actions[i], res);
-      done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
-    } else if (mode == MODE_RESET_SEEDED || mode == MODE_RESET_UNSEEDED) {
-      do_reset = mask == nullptr || mask[i] != 0;
-      if (do_reset && mode == MODE_RESET_SEEDED) v.spawn = 0;
-    }
-    if (mode == MODE_STEP) {
+      const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
       if (out.reward) out.reward[i] = res.reward;
       if (out.cost) out.cost[i] = res.cost;
       if (out.terminated) out.terminated[i] = (v.flags & kFlagTerminated) ? 1 : 0;
       if (out.truncated) out.truncated[i] = (v.flags & kFlagTruncated) ? 1 : 0;
       if (out.braking) out.braking[i] = (v.flags & kFlagBraking) ? 1 : 0;
+      my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
+    } else if (mode == MODE_RESET_SEEDED || mode == MODE_RESET_UNSEEDED) {
+      const bool do_reset = mask == nullptr || mask[i] != 0;
+      if (do_reset && mode == MODE_RESET_SEEDED) v.spawn = 0;
+      my_sel = do_reset ? 2 : 0;
     }
-    (void)do_reset;
-    sel[tid] = (mode == MODE_STEP && done && c.autoreset && err == 0) ? 1 : 0;
-    if (mode == MODE_RESET_SEEDED || mode == MODE_RESET_UNSEEDED) sel[tid] = do_reset ? 2 : 0;
   }
-  __syncthreads();
-  const bool any_final = __syncthreads_or(live && sel[tid] == 1);
-  if (mode == MODE_STEP && any_final && (out.final_obs || out.final_position)) {
-    // terminal observation of the envs that finished (gymnasium info["final_observation"])
-    ObsInfo oi;
-    if (live && sel[tid] == 1) {
-      build_obs(c, S, pl, v, masks, oi);
-      write_small_outputs(c, out, i, v, oi, true);
+  sel[tid] = my_sel;
+  STAMP(2);
+  const bool single = L.sub_envs >= nb;  // the whole workgroup's image fits: build once, rebuild resets
+  const int n_final = __syncthreads_count(my_sel == 1);
+  const bool want_final = mode == MODE_STEP && n_final && (out.final_obs || out.final_position || out.final_velocity);
+  if (single) {
+    if (live && (my_sel != 2)) {
+      ObsInfo oi;
+      build_obs(c, S, pl, v, st + tid * L.seg_words, oi);
+      write_small_outputs(c, out, i, v, oi, my_sel == 1);
     }
     __syncthreads();
-    if (out.final_obs) write_obs_block(c, out.final_obs, env0, nb, masks_all, L.mask_stride, sel);
-    __syncthreads();
+    if (want_final && out.final_obs)
+      write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
+                (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel);
+  } else if (want_final) {
+    obs_pass(c, S, pl, v, out, out.final_obs, env0, nb, my_sel == 1, true, sel, st, L);
   }
-  const bool reset_now = live && ((sel[tid] == 1) || (sel[tid] == 2));
+  STAMP(3);
+  const bool reset_now = my_sel != 0;
   const int n_resets = __syncthreads_count(reset_now);
   if (tid == 0 && n_resets) atomicAdd(&S.counters[1], (unsigned long long)n_resets);
-  if (live) {
-    if (reset_now) {
-      int e2 = env_reset(c, S, i, v, pl.p, q, par);
-      if (e2) err = e2;
-      // persist the new plan
-      uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
-      for (int k = 0; k < c.plan_stride / 8; k++) {
-        uint32_t wv[4];
+  if (reset_now) {
+    int e2 = env_reset(c, S, i, v, pl.p, q, par);
+    if (e2) err = e2;
+    uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
+    for (int k = 0; k < c.plan_stride / 8; k++) {
+      uint32_t wv[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) wv[j] = (k * 4 + j < L.plan_stride_dw) ? plan_w[k * 4 + j] : 0u;
-        dstp[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-      }
+      for (int j = 0; j < 4; j++) wv[j] = (k * 4 + j < L.plan_stride_dw) ? plan_w[k * 4 + j] : 0u;
+      dstp[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
     }
-    ObsInfo oi;
-    build_obs(c, S, pl, v, masks, oi);
-    write_small_outputs(c, out, i, v, oi, false);
+  }
+  STAMP(4);
+  if (live) {
     if (mode != MODE_OBSERVE) rec_store(S.rec, i, v);
     S.err[i] = (uint8_t)(-err);
   }
-  __syncthreads();
-  if (out.obs) write_obs_block(c, out.obs, env0, nb, masks_all, L.mask_stride, nullptr);
+  STAMP(5);
+  if (single) {
+    if (reset_now) {
+      ObsInfo oi;
+      build_obs(c, S, pl, v, st + tid * L.seg_words, oi);
+      write_small_outputs(c, out, i, v, oi, false);
+    }
+    __syncthreads();
+    if (out.obs)
+      write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
+                (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, nullptr);
+  } else {
+    obs_pass(c, S, pl, v, out, out.obs, env0, nb, live, false, nullptr, st, L);
+  }
   if (mode == MODE_STEP && tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
+  STAMP(6);
 }
 
 __global__ void k_random_actions(uint8_t* a, uint64_t n, uint64_t seed, uint64_t t) {
@@ -963,6 +1071,7 @@ struct pgtg_handle {
   hipStream_t stream = nullptr;
   DevCfg hcfg{};
   DevCfg* dcfg = nullptr;
+  Tables* dtab = nullptr;
   DevState S{};
   PgtgOutputs out{};
   Lds L{};
@@ -971,9 +1080,12 @@ struct pgtg_handle {
   std::string err;
   uint64_t seed_offset = 0;  // global index of env 0 (for sharded runs)
   bool timing = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool timed = false;
+  std::vector<hipEvent_t> evpool;  // pairs (start, stop) per timed launch
+  size_t ev_used = 0;
+  double acc_ms = 0.0;
+  uint64_t acc_n = 0;
 };
+
 
 static thread_local std::string g_create_err;
 
@@ -985,6 +1097,18 @@ static thread_local std::string g_create_err;
       return PGTG_E_DEVICE;                                                          \
     }                                                                                \
   } while (0)
+
+static int timing_flush(pgtg_handle* h) {
+  for (size_t k = 0; k + 1 < h->ev_used; k += 2) {
+    float ms = 0.f;
+    HIPCHK(h, hipEventSynchronize(h->evpool[k + 1]));
+    HIPCHK(h, hipEventElapsedTime(&ms, h->evpool[k], h->evpool[k + 1]));
+    h->acc_ms += ms;
+    h->acc_n++;
+  }
+  h->ev_used = 0;
+  return 0;
+}
 
 template <typename T>
 static int dalloc(pgtg_handle* h, T** p, size_t count) {
@@ -1093,6 +1217,8 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
         n++;
       }
     c.n_edges = n;
+    for (int k = 0; k < 4; k++) c.h0[k] = 0;
+    for (int e = 0; e < n; e++) c.h0[c.ed[e]] |= 1ull << c.ea[e];
     for (int e = 0; e < n; e++)
       for (int f = 0; f < n; f++)
         if (c.ea[f] == c.eb[e] && c.eb[f] == c.ea[e]) c.erev[e] = (uint8_t)f;
@@ -1270,14 +1396,42 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     S.cmp_tab = dc;
   }
 #undef ALLOC
+  {
+    Tables t;
+    memset(&t, 0, sizeof t);
+    memcpy(t.wall, hs::kTileWall, sizeof t.wall);
+    memcpy(t.seg, hs::kExitSeg, sizeof t.seg);
+    memcpy(t.obst, hs::kObstMask, sizeof t.obst);
+    memcpy(t.spawner, hs::kLaneSpawner, sizeof t.spawner);
+    memcpy(t.lanes, hs::kLanes, sizeof t.lanes);
+    memcpy(t.ind, c.ind_reward, sizeof t.ind);
+    memcpy(t.ea, c.ea, sizeof t.ea);
+    memcpy(t.eb, c.eb, sizeof t.eb);
+    memcpy(t.ed, c.ed, sizeof t.ed);
+    memcpy(t.erev, c.erev, sizeof t.erev);
+    memcpy(t.bt, c.bt, sizeof t.bt);
+    memcpy(t.bd, c.bd, sizeof t.bd);
+    if ((rc = dalloc(h, &h->dtab, 1)) || hipMemcpy(h->dtab, &t, sizeof t, hipMemcpyHostToDevice) != hipSuccess) {
+      g_create_err = "table upload failed";
+      pgtg_destroy(h);
+      return PGTG_E_DEVICE;
+    }
+  }
   if (hipMemcpy(h->dcfg, &h->hcfg, sizeof(DevCfg), hipMemcpyHostToDevice) != hipSuccess) {
     g_create_err = "config upload failed";
     pgtg_destroy(h);
     return PGTG_E_DEVICE;
   }
-  h->L = lds_layout(c);
+  {
+    // envs per 256-lane workgroup: small batches spread over more CUs with 4 lanes per env for
+    // the observation writes; large batches keep a full workgroup of env lanes for occupancy.
+    int envs = n_envs <= (uint64_t)64 * 1024 ? 64 : kBlock;
+    if (const char* e = getenv("PGTG_ENVS_PER_BLOCK")) envs = atoi(e);
+    if (envs != 64 && envs != 128 && envs != kBlock) envs = kBlock;
+    h->L = lds_layout(c, envs);
+  }
   h->lds = lds_bytes(h->L);
-  if (h->lds > 160 * 1024) {
+  if (h->lds + sizeof(Tables) > 160 * 1024) {
     g_create_err = "LDS budget exceeded";
     pgtg_destroy(h);
     return PGTG_E_UNSUPPORTED;
@@ -1291,8 +1445,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
 int pgtg_destroy(pgtg_handle* h) {
   if (!h) return PGTG_OK;
   for (void* p : h->allocs) (void)hipFree(p);
-  if (h->ev0) (void)hipEventDestroy(h->ev0);
-  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  for (auto e : h->evpool) (void)hipEventDestroy(e);
   delete h;
   return PGTG_OK;
 }
@@ -1311,20 +1464,25 @@ int pgtg_set_outputs(pgtg_handle* h, const PgtgOutputs* o) {
 
 static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, int mode) {
   HIPCHK(h, hipSetDevice(h->device));
-  uint64_t blocks = (h->n + kBlock - 1) / kBlock;
-  if (h->timing && mode == MODE_STEP) {
-    if (!h->ev0) {
-      HIPCHK(h, hipEventCreate(&h->ev0));
-      HIPCHK(h, hipEventCreate(&h->ev1));
+  uint64_t blocks = (h->n + h->L.envs - 1) / h->L.envs;
+  const bool timed = h->timing && mode == MODE_STEP;
+  if (timed) {
+    if (h->evpool.empty()) {
+      h->evpool.resize(2048);
+      for (auto& e : h->evpool) HIPCHK(h, hipEventCreate(&e));
     }
-    HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+    if (h->ev_used + 2 > h->evpool.size()) {
+      int rc = timing_flush(h);
+      if (rc) return rc;
+    }
+    HIPCHK(h, hipEventRecord(h->evpool[h->ev_used], h->stream));
   }
-  hipLaunchKernelGGL(k_env, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->S, actions, mask,
-                     h->out, mode, h->L);
+  hipLaunchKernelGGL(k_env, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S, actions,
+                     mask, h->out, mode, h->L);
   HIPCHK(h, hipGetLastError());
-  if (h->timing && mode == MODE_STEP) {
-    HIPCHK(h, hipEventRecord(h->ev1, h->stream));
-    h->timed = true;
+  if (timed) {
+    HIPCHK(h, hipEventRecord(h->evpool[h->ev_used + 1], h->stream));
+    h->ev_used += 2;
   }
   return PGTG_OK;
 }
@@ -1477,6 +1635,12 @@ int pgtg_error_count(pgtg_handle* h, uint64_t* n_errors, int32_t* first_code) {
   return PGTG_OK;
 }
 
+#ifdef PGTG_STAMPS
+int pgtg_read_stamps(uint64_t* out, uint64_t n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+}
+#endif
+
 int pgtg_window(const pgtg_handle* h) { return h ? h->hcfg.win : 0; }
 uint64_t pgtg_num_envs(const pgtg_handle* h) { return h ? h->n : 0; }
 const char* pgtg_last_error(const pgtg_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
@@ -1487,12 +1651,18 @@ int pgtg_enable_timing(pgtg_handle* h, int32_t on) {
   return PGTG_OK;
 }
 
-float pgtg_last_step_ms(pgtg_handle* h) {
-  if (!h || !h->timed) return -1.f;
-  float ms = -1.f;
-  if (hipEventSynchronize(h->ev1) != hipSuccess) return -1.f;
-  if (hipEventElapsedTime(&ms, h->ev0, h->ev1) != hipSuccess) return -1.f;
-  return ms;
+int pgtg_timing_read(pgtg_handle* h, double* total_ms, uint64_t* launches, int32_t reset) {
+  if (!h) return PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  int rc = timing_flush(h);
+  if (rc) return rc;
+  if (total_ms) *total_ms = h->acc_ms;
+  if (launches) *launches = h->acc_n;
+  if (reset) {
+    h->acc_ms = 0.0;
+    h->acc_n = 0;
+  }
+  return PGTG_OK;
 }
 
 }  // extern "C"

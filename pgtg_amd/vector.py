@@ -228,5 +228,8 @@ class PGTGVecEnv:
     def enable_timing(self, on: bool = True):
         self._lib.pgtg_enable_timing(self._h, int(on))
 
-    def last_step_ms(self) -> float:
-        return float(self._lib.pgtg_last_step_ms(self._h))
+    def timing_read(self, reset: bool = True) -> tuple[float, int]:
+        """(summed step-kernel ms, timed launches) from HIP events on the handle's stream."""
+        ms, n = C.c_double(), C.c_uint64()
+        _check(self._lib.pgtg_timing_read(self._h, C.byref(ms), C.byref(n), int(reset)), self._h)
+        return ms.value, n.value
