@@ -104,14 +104,16 @@ def main():
     if rank == 0 and world == 1:
         build()
     from pgtg_amd.config import make_spec
+    from pgtg_amd.dist import Shard, reduce_counters
     from pgtg_amd.vector import PGTGVecEnv
 
     cfg_idx, desc, n_local, kwargs = WORKLOADS[args.workload]
     if args.envs:
         n_local = args.envs
     spec = make_spec(**kwargs)
+    shard = Shard(rank, world, n_local)
     env = PGTGVecEnv(n_local, spec=spec, device=local, autoreset=True)
-    env.reset(seed=rank * n_local)  # global env g = rank*n_local + i gets seed g
+    env.reset(seed=shard.offset)  # global env g = rank*n_local + i gets seed g
     act_seed = 0x5EED
     for t in range(args.warmup):
         env.step_random(act_seed, t)
@@ -131,14 +133,8 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms, launches = env.timing_read(reset=True)
     steps1, eps1 = env.counters()
-    # RCCL: global env-step / episode counters (sum) and the slowest rank's time (max)
-    cnt = torch.tensor([steps1 - steps0, eps1 - eps0], dtype=torch.int64, device=dev)
-    tim = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tim, op=dist.ReduceOp.MAX)
-    total_steps, total_eps = int(cnt[0].item()), int(cnt[1].item())
-    t_max = float(tim[0].item())
+    # RCCL (nccl backend) all-reduce: global env-step / episode counters (sum), slowest rank's time (max)
+    total_steps, total_eps, t_max = reduce_counters(steps1 - steps0, eps1 - eps0, elapsed, device=dev)
     value = total_steps / t_max
 
     if rank == 0:
