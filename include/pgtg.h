@@ -108,6 +108,7 @@ typedef struct {
   /* vector-env options (no reference equivalent; pgtg/train.py:21-41 wraps with TimeLimit) */
   int32_t autoreset;                   /* 1: same-step auto-reset (gymnasium/SB3 vector semantics) */
   int32_t max_episode_steps;           /* TimeLimit truncation, 0 = none */
+  int32_t min_car_capacity;            /* car slots per env for pgtg_add_car (tests), 0 = from density */
 } PgtgConfig;
 
 /* Output buffers (device pointers, caller-owned, contiguous).  NULL = not produced. */

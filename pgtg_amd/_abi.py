@@ -61,7 +61,7 @@ class PgtgConfig(C.Structure):
         ("fixed_map", C.c_int32), ("fm_w", C.c_int32), ("fm_h", C.c_int32),
         ("fm_exits", C.c_uint8 * MAX_TILES), ("fm_obst_type", C.c_int8 * MAX_TILES),
         ("fm_obst_mask", C.c_int8 * MAX_TILES), ("fm_start", C.c_int32 * 3), ("fm_goal", C.c_int32 * 3),
-        ("autoreset", C.c_int32), ("max_episode_steps", C.c_int32),
+        ("autoreset", C.c_int32), ("max_episode_steps", C.c_int32), ("min_car_capacity", C.c_int32),
     ]
 
 
@@ -129,7 +129,8 @@ def lib():
     return L
 
 
-def config_struct(spec: "cfgmod.EnvSpec", autoreset: bool, max_episode_steps: int | None) -> PgtgConfig:
+def config_struct(spec: "cfgmod.EnvSpec", autoreset: bool, max_episode_steps: int | None,
+                  min_car_capacity: int = 0) -> PgtgConfig:
     c = PgtgConfig()
     c.abi_version = PGTG_ABI_VERSION
     c.width, c.height = spec.width, spec.height
@@ -183,4 +184,5 @@ def config_struct(spec: "cfgmod.EnvSpec", autoreset: bool, max_episode_steps: in
             c.fm_goal[i] = fm.goal[i]
     c.autoreset = int(autoreset)
     c.max_episode_steps = int(max_episode_steps or 0)
+    c.min_car_capacity = int(min_car_capacity)
     return c

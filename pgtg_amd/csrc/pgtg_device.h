@@ -66,7 +66,15 @@ struct DevCfg {
   int32_t need_car, need_ice, need_broken, need_sand;
   double density;
   double profile_cdf[5];
-  int32_t car_cap;
+  int32_t car_cap;      // car slots per env and bank
+  int32_t max_spawners; // spawner list capacity per env (nt * 5)
+  // DRIVER_BEHAVIORS (pgtg/environment.py:64-109) in DriverProfile order, thresholds precomputed
+  double beh_yellow[5], beh_red[5], beh_one_minus_patience[5], beh_speed[5], beh_delay[5];
+  int32_t beh_min_follow[5], beh_patience_thr[5];  // patience > level*10  <=>  patience > floor(level*10)
+  int32_t traf_bytes;      // per-lane LDS traffic region (occupancy counters / reset scratch)
+  int32_t floyd_seen_off;  // byte offsets inside it used during traffic_reset
+  int32_t floyd_pre_off;
+  int32_t manual_cars;     // cars may be added through pgtg_add_car
   int32_t n_rules;
   PgtgRule rules[PGTG_MAX_RULES];
   int32_t nsd_off, nsd_pitch;   // nsd table index (dx+off)*pitch + (dy+off)
@@ -88,6 +96,16 @@ struct Tables {
   uint8_t ea[kMaxEdges], eb[kMaxEdges], ed[kMaxEdges], erev[kMaxEdges];
   uint8_t bt[kMaxBorder], bd[kMaxBorder];
   uint32_t lanes[16][81];   // kLanes (copied only when traffic or lane/spawner channels need it)
+  // traffic tables (copied with lanes): lane-square slot per square (255 = none), square per slot,
+  // per-column masks (bit ly) of lane squares, lane-data spawners and the four "all" lanes
+  uint8_t li[16][81];
+  uint8_t slot_sq[16][32];
+  uint16_t lanecol[16][9];
+  uint16_t spcol[16][9];
+  uint16_t allcol[16][4][9];
+  uint8_t lane_route[32];
+  uint8_t route_type_lane[20][4];
+  uint8_t rule_w[PGTG_MAX_RULES][6][20];
 };
 
 // one PCG64 stream, SoA over envs
@@ -106,9 +124,14 @@ struct DevState {
   uint16_t* plan;         // [n][plan_stride]
   DevStream car, ice, broken, sand;
   uint32_t* visited;      // [n][vis_words] or null
-  uint32_t* cars;         // [n][car_cap][2] packed cars or null (traffic)
-  uint32_t* car_ids;      // [n][car_cap]
-  uint32_t* car_meta;     // [n]: n_cars | next_car_id (2 x u32)
+  // traffic: two banks of car slots, car-major / env-minor ([bank][slot][n]) so that the lanes of a
+  // wave read slot k of 64 envs with one coalesced access.  w0 = x | y<<8 | route<<16 | profile<<21 |
+  // delay<<24, w1 = patience counter, id = car id.  traf[n] = {n_cars | n_spawners<<16, next_id, bank, 0}
+  uint32_t* car_w0;
+  uint32_t* car_w1;
+  uint32_t* car_id;
+  uint4* traf;
+  uint16_t* spawners;     // [max_spawners][n] square codes x | y<<8, x-major order
   uint8_t* err;           // [n] last error code (negated PGTG_E_*)
   unsigned long long* counters;  // [2]: env steps, episodes
   const int8_t* nsd_tab;

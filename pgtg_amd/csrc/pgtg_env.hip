@@ -161,6 +161,46 @@ __device__ __forceinline__ int phase_color(const DevCfg& c, uint32_t ph) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// traffic helpers: occupancy counters per lane square in LDS (tile t, lane slot li -> t*32 + li)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_slot(const DevCfg& c, const Plan& pl, int x, int y) {
+  int tx = x / kTile, ty = y / kTile;
+  int lx = x - tx * kTile, ly = y - ty * kTile;
+  int t = ty * c.tw + tx;
+  uint32_t ex = plan_exits(pl[t]);
+  int li = ex ? sT.li[ex][lx * 9 + ly] : 255;
+  return li == 255 ? -1 : t * 32 + li;
+}
+__device__ __forceinline__ bool square_tlight(const DevCfg& c, const Plan& pl, int x, int y) {
+  int tx = x / kTile, ty = y / kTile;
+  int lx = x - tx * kTile, ly = y - ty * kTile;
+  uint32_t p = pl[ty * c.tw + tx];
+  int sq = lx * 9 + ly;
+  return plan_otype(p) == 4 && !bit81(sT.wall[plan_exits(p)], sq) && bit81(sT.obst[plan_omask(p)], sq);
+}
+__device__ __forceinline__ int occ_at(const DevCfg& c, const Plan& pl, const uint8_t* occ, int x, int y) {
+  int s = lane_slot(c, pl, x, y);
+  return s < 0 ? 0 : occ[s];
+}
+// returns false on counter overflow (more than 255 cars on one square)
+__device__ __forceinline__ bool occ_inc(uint8_t* occ, int s) {
+  if (occ[s] == 255) return false;
+  occ[s]++;
+  return true;
+}
+__device__ __forceinline__ int kth_bit(uint32_t m, int k) {
+  for (int j = 0; j < k; j++) m &= m - 1u;
+  return __ffs((int)m) - 1;
+}
+
+struct CarStore {  // one env's view of the car banks
+  uint32_t *w0, *w1, *id;
+  uint64_t n;  // stride between slots (= number of envs)
+  uint64_t i;  // env index
+  __device__ __forceinline__ uint64_t at(int bank, int cap, int k) const { return ((uint64_t)bank * cap + k) * n + i; }
+};
+
+// ------------------------------------------------------------------------------------------------
 // reset: seeding, procedural map, compilation, start square  (pgtg/environment.py:581-656)
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void rand_pos(const DevCfg& c, Pcg& r, int& x, int& y) {  // map_generator.py:602-626
@@ -428,15 +468,132 @@ __device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, uin
   return len;
 }
 
+struct TrafState {
+  uint32_t n_cars, n_spawners, next_id, bank;
+};
+
+// spawner squares of local column lx of tile (tx, ty): lane-data spawners (dead ends) plus the
+// border rule of pgtg/parser.py:120-148 ("car_lane all right" on the west border, ...)
+__device__ __forceinline__ uint32_t spawner_colmask(const DevCfg& c, uint32_t ex, int tx, int ty, int lx) {
+  if (!ex) return 0u;
+  uint32_t m = sT.spcol[ex][lx];
+  if (tx == 0) m |= sT.allcol[ex][3][lx];
+  if (tx == c.tw - 1) m |= sT.allcol[ex][2][lx];
+  if (ty == 0) m |= sT.allcol[ex][1][lx];
+  if (ty == c.th - 1) m |= sT.allcol[ex][0][lx];
+  return m;
+}
+
+// Initial traffic of a fresh episode (EpisodeMap scans pgtg/map.py:31-42 and
+// _create_initial_traffic pgtg/environment.py:830-879).  `tr` is the lane's LDS traffic region:
+// Floyd's output/seen set and the column prefix alias the occupancy counters, which are rebuilt
+// from the new cars at the end.
+__device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S, uint64_t i, const Plan& pl,
+                                             Pcg& cr, uint8_t* tr, TrafState& ts) {
+  const uint64_t N = S.n;
+  // car spawners in x-major order -> HBM list
+  int nsp = 0;
+  for (int x = 0; x < c.W; x++) {
+    int tx = x / kTile, lx = x - tx * kTile;
+    for (int ty = 0; ty < c.th; ty++) {
+      uint32_t m = spawner_colmask(c, plan_exits(pl[ty * c.tw + tx]), tx, ty, lx);
+      while (m) {
+        int ly = __ffs((int)m) - 1;
+        m &= m - 1u;
+        if (nsp < c.max_spawners) S.spawners[(uint64_t)nsp * N + i] = (uint16_t)(x | (ty * kTile + ly) << 8);
+        nsp++;
+      }
+    }
+  }
+  // spawnable positions (squares holding any car lane), x-major: per-column prefix counts
+  uint16_t* colpre = reinterpret_cast<uint16_t*>(tr + c.floyd_pre_off);
+  int np = 0;
+  for (int x = 0; x < c.W; x++) {
+    int tx = x / kTile, lx = x - tx * kTile;
+    colpre[x] = (uint16_t)np;
+    for (int ty = 0; ty < c.th; ty++) {
+      uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
+      if (ex) np += __popc(sT.lanecol[ex][lx]);
+    }
+  }
+  colpre[c.W] = (uint16_t)np;
+  const int ncars = (int)((double)np * c.density);  // int(len(positions) * traffic_density)
+  int k = 0;
+  CarStore cs{S.car_w0, S.car_w1, S.car_id, N, i};
+  if (ncars > 0 && np > 0) {
+    k = min(ncars, np);
+    if (k > c.car_cap) return PGTG_E_UNSUPPORTED;
+    uint16_t* out = reinterpret_cast<uint16_t*>(tr);
+    uint32_t* seen = reinterpret_cast<uint32_t*>(tr + c.floyd_seen_off);
+    for (int w = 0; w < (np + 31) / 32; w++) seen[w] = 0u;
+    // Generator.choice(np, k, replace=False): Floyd's algorithm, then _shuffle_int
+    for (int j = np - k; j < np; j++) {
+      int val = (int)pcg_int(cr, (uint32_t)(j + 1));
+      if ((seen[val >> 5] >> (val & 31)) & 1u) val = j;
+      seen[val >> 5] |= 1u << (val & 31);
+      out[j - (np - k)] = (uint16_t)val;
+    }
+    for (int m = k - 1; m >= 1; m--) {
+      int jj = (int)pcg_int(cr, (uint32_t)(m + 1));
+      uint16_t t = out[m];
+      out[m] = out[jj];
+      out[jj] = t;
+    }
+    for (int m = 0; m < k; m++) {
+      int idx = out[m];
+      // x: last column whose prefix <= idx
+      int lo = 0, hi = c.W;  // colpre[lo] <= idx < colpre[hi]
+      while (hi - lo > 1) {
+        int mid = (lo + hi) >> 1;
+        if (colpre[mid] <= idx) lo = mid; else hi = mid;
+      }
+      int x = lo, rr = idx - colpre[x], tx = x / kTile, lx = x - tx * kTile, y = 0;
+      for (int ty = 0; ty < c.th; ty++) {
+        uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
+        uint32_t msk = ex ? sT.lanecol[ex][lx] : 0u;
+        int cnt = __popc(msk);
+        if (rr < cnt) {
+          y = ty * kTile + kth_bit(msk, rr);
+          break;
+        }
+        rr -= cnt;
+      }
+      uint32_t rl = square_lanes(c, pl, x, y) & 0x0fffffffu;
+      int nr = __popc(rl);
+      if (nr == 0) return PGTG_E_MAP;  // "a car was spawned on a field where no car lane was found"
+      int prof = pcg_choice_cdf<5>(cr, c.profile_cdf);
+      int route = sT.lane_route[kth_bit(rl, (int)pcg_int(cr, (uint32_t)nr))];
+      uint64_t a = cs.at(0, c.car_cap, m);
+      cs.w0[a] = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
+      cs.w1[a] = 0u;
+      cs.id[a] = (uint32_t)m;
+    }
+  }
+  ts.n_cars = (uint32_t)k;
+  ts.n_spawners = (uint32_t)min(nsp, c.max_spawners);
+  ts.next_id = (uint32_t)k;
+  ts.bank = 0;
+  // occupancy counters of the new cars
+  for (int w = 0; w < c.nt * 8; w++) reinterpret_cast<uint32_t*>(tr)[w] = 0u;
+  for (int m = 0; m < k; m++) {
+    uint32_t a = cs.w0[cs.at(0, c.car_cap, m)];
+    int sl = lane_slot(c, pl, (int)(a & 255u), (int)((a >> 8) & 255u));
+    if (sl < 0 || !occ_inc(tr, sl)) return PGTG_E_UNSUPPORTED;
+  }
+  return 0;
+}
+
 // The full per-env reset.  `key` = spawn counter (5 children per episode).  Returns 0 or -code.
-__device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, uint16_t* plan, uint8_t* q,
-                         uint8_t* par) {
+template <bool TR>
+__device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, uint16_t* plan,
+                                         uint8_t* q, uint8_t* par, uint8_t* tr, TrafState& ts) {
   STAMP(8);
   uint64_t seed = S.seed[i];
   SeedPool sp = ss_pool(seed);
   uint32_t k = v.spawn;
   Pcg map_rng = ss_child(sp, k + 0u);
-  if (c.need_car) stream_store_all(S.car, i, ss_child(sp, k + 1u));
+  Pcg car_rng;
+  if ((TR && c.need_car)) car_rng = ss_child(sp, k + 1u);
   if (c.need_ice) stream_store_all(S.ice, i, ss_child(sp, k + 2u));
   if (c.need_broken) stream_store_all(S.broken, i, ss_child(sp, k + 3u));
   if (c.need_sand) stream_store_all(S.sand, i, ss_child(sp, k + 4u));
@@ -483,6 +640,12 @@ __device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uin
     for (int q2 = 0; q2 < c.vis_words; q2++) vis[q2] = 0;
     int b = (v.px + 2) * c.vis_pitch + (v.py + 2);
     vis[b >> 5] |= 1u << (b & 31);
+  }
+  if ((TR && c.need_car)) {
+    Plan pl{plan};
+    int e = traffic_reset(c, S, i, pl, car_rng, tr, ts);
+    stream_store_all(S.car, i, car_rng);
+    if (e) return e;
   }
   return 0;
 }
@@ -554,8 +717,9 @@ __device__ __forceinline__ bool nearest_goal_square(const DevCfg& c, const Plan&
 
 // Observation of one env into its LDS segments: channel ci occupies words seg[ci*MW .. +MW) with
 // bit b = window square b (row-major over x, then y), unused high bits zero.  Plain stores only.
+template <bool TR>
 __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
-                                          uint32_t* seg, ObsInfo& oi) {
+                                          uint32_t* seg, ObsInfo& oi, const uint8_t* occ) {
   int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
   int tx = pix / kTile, ty = piy / kTile;
   int color = phase_color(c, v.phase);
@@ -581,6 +745,15 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
     int st_t = (int)(v.sg & 0xffu), st_d = (int)((v.sg >> 8) & 0xffu);
     int gl_t = (int)((v.sg >> 16) & 0xffu), gl_d = (int)(v.sg >> 24);
     uint32_t ot = plan_otype(p);
+    uint32_t CR[3] = {0, 0, 0};  // squares of this tile holding a car
+    if ((TR && c.need_car) && ex) {
+      for (int sl = 0; sl < 32; sl++) {
+        if (occ[t * 32 + sl]) {
+          int sq = sT.slot_sq[ex][sl];
+          CR[sq >> 5] |= 1u << (sq & 31);
+        }
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       W3[k] = sT.wall[ex][k];
@@ -608,7 +781,8 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
           case PGTG_CH_ICE: val = ot == 1 ? OB[k] : 0u; break;
           case PGTG_CH_BROKEN: val = ot == 2 ? OB[k] : 0u; break;
           case PGTG_CH_SAND: val = ot == 3 ? OB[k] : 0u; break;
-          default: val = 0u; break;  // PGTG_CH_ZERO, PGTG_CH_TRAFFIC (filled by the traffic pass)
+          case PGTG_CH_TRAFFIC: val = CR[k]; break;
+          default: val = 0u; break;  // PGTG_CH_ZERO
         }
         out3[k] = val;
       }
@@ -622,7 +796,16 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
       int code = c.channels[ci];
       for (int w0 = 0; w0 < WW; w0 += 32) {
         uint32_t acc = 0;
-        if (code != PGTG_CH_ZERO && code != PGTG_CH_TRAFFIC) {
+        if (code == PGTG_CH_TRAFFIC) {
+          if ((TR && c.need_car)) {
+            int nb = min(32, WW - w0);
+            for (int b = 0; b < nb; b++) {
+              int bb = w0 + b, ii = bb / win, j = bb - ii * win;
+              int x = oi.x0 + ii, y = oi.y0 + j;
+              if (inside(c, x, y) && occ_at(c, pl, occ, x, y) > 0) acc |= 1u << b;
+            }
+          }
+        } else if (code != PGTG_CH_ZERO) {
           int nb = min(32, WW - w0);
           for (int b = 0; b < nb; b++) {
             int bb = w0 + b, i = bb / win, j = bb - i * win;
@@ -665,23 +848,208 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
 __device__ __forceinline__ int acc_x(int a) { return a / 3 - 1; }
 __device__ __forceinline__ int acc_y(int a) { return a % 3 - 1; }
 
+// Traffic tick: every car of the tick-start list, in list order (pgtg/environment.py:1121-1127,
+// _get_next_car_position_and_route :881-968, _should_car_move :678-691, traffic lights :664-676,
+// _spawn_new_car :970-1002).  Survivors go to the other bank in order, respawned cars are appended
+// after them in creation order; occupancy counters follow every move so later cars see earlier ones.
+__device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uint64_t i, const EnvView& v,
+                                         const Plan& pl, uint8_t* occ, TrafState& ts, Pcg& cr, int color) {
+  CarStore cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
+  const int cap = c.car_cap, cur = (int)ts.bank, nxt = cur ^ 1;
+  const int n0 = (int)ts.n_cars;
+  int w = 0, nnew = 0;
+  for (int r = 0; r < n0; r++) {
+    const uint64_t ar = cs.at(cur, cap, r);
+    const uint32_t a = cs.w0[ar];
+    uint32_t pat = cs.w1[ar];
+    const uint32_t id = cs.id[ar];
+    const int x = (int)(a & 255u), y = (int)((a >> 8) & 255u), prof = (int)((a >> 21) & 7u);
+    int route = (int)((a >> 16) & 31u), delay = (int)((a >> 24) & 3u);
+    int nx = x, ny = y;
+    bool remove = false;
+    bool move;
+    if (delay > 0) {
+      delay -= 1;
+      move = false;
+    } else if (pcg_double(cr) < c.beh_delay[prof]) {
+      delay = 1 + (int)pcg_int(cr, 3);  // integers(1, 4)
+      move = false;
+    } else {
+      move = pcg_double(cr) < c.beh_speed[prof];
+    }
+    if (!move) {
+      pat += 1;
+    } else {
+      bool decided = false;
+      for (int t = 0; t < 4 && !decided; t++) {  // up, down, left, right
+        const int px = x + (t == 2 ? -1 : t == 3 ? 1 : 0), py = y + (t == 0 ? -1 : t == 1 ? 1 : 0);
+        if (!inside(c, px, py)) continue;
+        const uint32_t ln = square_lanes(c, pl, px, py);
+        if ((ln >> (28 + t)) & 1u) {  // "car_lane all <type>": enter with a new random route
+          const uint32_t rl = ln & 0x0fffffffu;
+          const int nr = __popc(rl);
+          if (nr == 0) return PGTG_E_MAP;  // numpy choice([]) raises
+          route = sT.lane_route[kth_bit(rl, (int)pcg_int(cr, (uint32_t)nr))];
+          pat = 0;
+          nx = px;
+          ny = py;
+          decided = true;
+        } else {
+          const int lane = sT.route_type_lane[route][t];
+          if (lane != 255 && ((ln >> lane) & 1u)) {
+            decided = true;
+            bool stop = false;
+            if (square_tlight(c, pl, px, py)) {
+              if (color == 1) stop = pcg_double(cr) < c.beh_yellow[prof];
+              else if (color == 2) stop = pcg_double(cr) >= c.beh_red[prof];
+            }
+            if (stop) {
+              pat += 1;
+            } else if (occ_at(c, pl, occ, px, py) > 0) {
+              bool go = false;
+              if (c.beh_min_follow[prof] == 0 || (int)pat > c.beh_patience_thr[prof])
+                go = pcg_double(cr) < c.beh_one_minus_patience[prof];
+              if (go) {
+                pat = 0;
+                nx = px;
+                ny = py;
+              } else {
+                pat += 1;
+              }
+            } else {
+              pat = 0;
+              nx = px;
+              ny = py;
+            }
+          }
+        }
+      }
+      if (!decided) {
+        pat += 1;
+        remove = true;
+      }
+    }
+    const int s_old = lane_slot(c, pl, x, y);
+    if (remove) {
+      occ[s_old]--;
+      // _spawn_new_car: choice(car_spawners) -> sorted routes -> profile -> route
+      int sx = 0, sy = 0;
+      if (ts.n_spawners > 0) {
+        uint32_t code = S.spawners[(uint64_t)pcg_int(cr, ts.n_spawners) * S.n + i];
+        sx = (int)(code & 255u);
+        sy = (int)(code >> 8);
+      }
+      const uint32_t rl = square_lanes(c, pl, sx, sy) & 0x0fffffffu;
+      const int nr = __popc(rl);
+      const int nprof = pcg_choice_cdf<5>(cr, c.profile_cdf);
+      if (nr == 0) return PGTG_E_MAP;
+      const int nroute = sT.lane_route[kth_bit(rl, (int)pcg_int(cr, (uint32_t)nr))];
+      const uint64_t an = cs.at(nxt, cap, n0 - 1 - nnew);
+      cs.w0[an] = (uint32_t)sx | (uint32_t)sy << 8 | (uint32_t)nroute << 16 | (uint32_t)nprof << 21;
+      cs.w1[an] = 0u;
+      cs.id[an] = ts.next_id++;
+      nnew++;
+      const int s_new = lane_slot(c, pl, sx, sy);
+      if (s_new < 0 || !occ_inc(occ, s_new)) return PGTG_E_UNSUPPORTED;
+    } else {
+      if (nx != x || ny != y) {
+        occ[s_old]--;
+        if (!occ_inc(occ, lane_slot(c, pl, nx, ny))) return PGTG_E_UNSUPPORTED;
+      }
+      const uint64_t aw = cs.at(nxt, cap, w);
+      cs.w0[aw] = (uint32_t)nx | (uint32_t)ny << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21 | (uint32_t)delay << 24;
+      cs.w1[aw] = pat;
+      cs.id[aw] = id;
+      w++;
+    }
+  }
+  // respawned cars were written from the end backwards: restore creation order
+  for (int j = 0; j < nnew / 2; j++) {
+    const uint64_t p1 = cs.at(nxt, cap, w + j), p2 = cs.at(nxt, cap, n0 - 1 - j);
+    uint32_t t0 = cs.w0[p1], t1 = cs.w1[p1], t2 = cs.id[p1];
+    cs.w0[p1] = cs.w0[p2];
+    cs.w1[p1] = cs.w1[p2];
+    cs.id[p1] = cs.id[p2];
+    cs.w0[p2] = t0;
+    cs.w1[p2] = t1;
+    cs.id[p2] = t2;
+  }
+  ts.bank = (uint32_t)nxt;
+  return 0;
+}
+
+// TrafficRuleEngine.apply_braking (pgtg/environment.py:226-294) on the agent's (clamped) tile after
+// the cars moved; returns true if any rule triggers.  hist: per-lane LDS route histogram (20 B).
+__device__ __forceinline__ bool apply_braking(const DevCfg& c, const DevState& S, uint64_t i, const EnvView& v,
+                                              const Plan& pl, const TrafState& ts, uint8_t* hist) {
+  const int tx = min(max((int)floorf((float)v.px / kTile), 0), c.tw - 1);
+  const int ty = min(max((int)floorf((float)v.py / kTile), 0), c.th - 1);
+  const uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
+  const int s2 = v.vx * v.vx + v.vy * v.vy;
+  uint32_t cand = 0;
+  for (int r = 0; r < c.n_rules; r++)
+    if (c.rules[r].tile_exits == (int)ex && s2 >= c.rules[r].speed_sq_min && s2 <= c.rules[r].speed_sq_max)
+      cand |= 1u << r;
+  if (!cand) return false;
+  // traffic in the tile: count + route histogram
+  CarStore cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
+  for (int r = 0; r < 20; r++) hist[r] = 0;
+  int n_in = 0;
+  for (int k = 0; k < (int)ts.n_cars; k++) {
+    uint32_t a = cs.w0[cs.at((int)ts.bank, c.car_cap, k)];
+    int x = (int)(a & 255u), y = (int)((a >> 8) & 255u);
+    if (x / kTile == tx && y / kTile == ty) {
+      n_in++;
+      hist[(a >> 16) & 31u]++;
+    }
+  }
+  // agent direction from the subgoal compass (environment.py:185-206, 1037-1090)
+  int dir;
+  int bx = 0, by = 0;
+  int cp = -1;
+  if (nearest_goal_square(c, pl, v, v.px, v.py, bx, by))
+    cp = S.cmp_tab[(bx - v.px + c.cmp_off) * c.cmp_pitch + (by - v.py + c.cmp_off)];
+  if (cp >= 0) dir = cp >> 1;  // N,NE -> south_to_north; E,SE -> west_to_east; S,SW; W,NW
+  else dir = s2 == 0 ? 4 : 5;  // "stationary" (speed < 0.1) / "near_goal"
+  for (int r = 0; r < c.n_rules; r++) {
+    if (!((cand >> r) & 1u)) continue;
+    if (n_in < c.rules[r].min_traffic) continue;
+    int match = 0;
+    for (int q = 0; q < 20; q++) match += hist[q] * (int)sT.rule_w[r][dir][q];
+    if (match >= c.rules[r].min_matching_traffic) return true;
+  }
+  return false;
+}
+
 struct StepResult {
   double reward, cost;
 };
 
-__device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, const Plan& pl, int action,
-                        StepResult& res) {
+template <bool TR>
+__device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, const Plan& pl,
+                                        int action, StepResult& res, uint8_t* occ, TrafState& ts, uint8_t* hist) {
   res.reward = 0.0;
   res.cost = 0.0;
   if (v.flags & (kFlagTerminated | kFlagTruncated)) return PGTG_E_DONE;
   if ((unsigned)action > 8u) return PGTG_E_INVALID;
   v.phase = (v.phase + 1u) % (uint32_t)c.phase_total;
   const int ax = acc_x(action), ay = acc_y(action);
+  // cars move first (environment.py:1120-1127), with this tick's light phase
+  if ((TR && c.need_car) && ts.n_cars > 0) {
+    Pcg cr = stream_load(S.car, i);
+    int e = move_cars(c, S, i, v, pl, occ, ts, cr, phase_color(c, v.phase));
+    stream_store_state(S.car, i, cr);
+    if (e) return e;
+  }
   double reward = 0.0, perf = 0.0, cost = 0.0;
   int cx = v.px, cy = v.py;
   v.vx += ax;
   v.vy += ay;
   v.flags &= ~kFlagBraking;
+  if (TR && c.n_rules > 0 && apply_braking(c, S, i, v, pl, ts, hist)) {  // environment.py:1145
+    v.vx = v.vy = 0;
+    v.flags |= kFlagBraking;
+  }
   if (abs(v.vx) > 30000 || abs(v.vy) > 30000) return PGTG_E_UNSUPPORTED;
   Pcg ice, broken, sand;
   if (c.need_ice) ice = stream_load(S.ice, i);
@@ -707,7 +1075,7 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
       break;
     }
     uint32_t f = square_flags(c, pl, v, cx, cy);
-    if (f & SQ_WALL) {
+    if ((f & SQ_WALL) || ((TR && c.need_car) && !c.ignore_collisions && occ_at(c, pl, occ, cx, cy) > 0)) {
       if (c.separate_cost) cost += c.crash_penalty; else reward -= c.crash_penalty;
       v.flags |= kFlagTerminated;
       break;
@@ -866,6 +1234,8 @@ struct Lds {
   int envs;            // envs per workgroup (<= kBlock); lanes >= envs only help with the writes
   int plan_stride_dw;  // per-lane plan words (odd)
   int scratch_dw;      // per-lane BFS scratch words (odd)
+  int traf_dw;         // per-lane traffic region words (occupancy counters / reset scratch), odd or 0
+  int hist_dw;         // per-lane route histogram words for the braking rules, odd or 0
   int seg_words;       // per-env observation words (n_channels * mask_words)
   int sub_envs;        // envs per observation sub-batch (== envs when they all fit)
   int stream_words;    // observation image words (+2 pad)
@@ -878,6 +1248,8 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.envs = envs;
   l.plan_stride_dw = odd_up((c.nt + 1) / 2);
   l.scratch_dw = odd_up((2 * c.nt + 3) / 4);
+  l.traf_dw = c.need_car ? odd_up(c.traf_bytes / 4) : 0;
+  l.hist_dw = c.n_rules > 0 ? 5 : 0;
   l.seg_words = c.n_channels * c.mask_words;
   const int budget_words = 12 * 1024;  // 48 KiB observation image
   int sub = l.seg_words > 0 ? (budget_words - 2) / l.seg_words : envs;
@@ -886,7 +1258,8 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   return l;
 }
 __host__ inline size_t lds_bytes(const Lds& l) {
-  return (size_t)4 * ((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw) + l.stream_words) + kBlock;
+  return (size_t)4 * ((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
+         kBlock;
 }
 
 enum { MODE_STEP = 0, MODE_RESET_SEEDED = 1, MODE_RESET_UNSEEDED = 2, MODE_OBSERVE = 3 };
@@ -906,15 +1279,17 @@ __device__ __forceinline__ void write_small_outputs(const DevCfg& c, const PgtgO
 
 // Observation pass over sub-batches: build the envs with want != 0 (small outputs as final or not)
 // into the segment image, then write the image slice to dst (selection sel).
+template <bool TR>
 __device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
                                          const PgtgOutputs& o, uint8_t* dst, uint64_t env0, int nb, bool want,
-                                         bool final, const uint8_t* sel, uint32_t* st, const Lds& L) {
+                                         bool final, const uint8_t* sel, uint32_t* st, const Lds& L,
+                                         const uint8_t* occ) {
   const int tid = threadIdx.x;
   for (int sb = 0; sb < nb; sb += L.sub_envs) {
     const int cnt = min(L.sub_envs, nb - sb);
     if (want && tid >= sb && tid < sb + cnt) {
       ObsInfo oi;
-      build_obs(c, S, pl, v, st + (tid - sb) * L.seg_words, oi);
+      build_obs<TR>(c, S, pl, v, st + (tid - sb) * L.seg_words, oi, occ);
       write_small_outputs(c, o, env0 + tid, v, oi, final);
     }
     __syncthreads();
@@ -925,7 +1300,9 @@ __device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, con
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
+// 4 waves per SIMD (<= 128 VGPRs) keeps 16 waves per CU resident to hide per-lane latency
+template <bool TR>
+__global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
                                                  DevState S, const uint8_t* __restrict__ actions,
                                                  const uint8_t* __restrict__ mask, PgtgOutputs out, int mode, Lds L) {
   extern __shared__ uint32_t lds[];
@@ -934,7 +1311,7 @@ __global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, 
   STAMP(0);
   // stage the lane-indexed tables (kLanes only when a pass needs it)
   {
-    const int words = (int)((offsetof(Tables, lanes) + (c.generic_channels || c.need_car ? sizeof(sT.lanes) : 0)) / 4);
+    const int words = (int)((c.generic_channels || (TR && c.need_car) ? sizeof(Tables) : offsetof(Tables, lanes)) / 4);
     const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
     uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
     for (int k = tid; k < words; k += blockDim.x) dstt[k] = src[k];
@@ -943,19 +1320,31 @@ __global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, 
   const int nb = (int)min((uint64_t)L.envs, S.n - env0);
   const uint64_t i = env0 + tid;
   const bool live = tid < nb;
-  const int lane_slot = tid < L.envs ? tid : 0;
-  uint32_t* plan_w = lds + lane_slot * L.plan_stride_dw;
-  uint32_t* scr_w = lds + L.envs * L.plan_stride_dw + lane_slot * L.scratch_dw;
-  uint32_t* st = lds + L.envs * (L.plan_stride_dw + L.scratch_dw);
+  const int my_slot = tid < L.envs ? tid : 0;
+  uint32_t* plan_w = lds + my_slot * L.plan_stride_dw;
+  uint32_t* scr_w = lds + L.envs * L.plan_stride_dw + my_slot * L.scratch_dw;
+  uint32_t* traf_w = lds + L.envs * (L.plan_stride_dw + L.scratch_dw) + my_slot * L.traf_dw;
+  uint32_t* hist_w = lds + L.envs * (L.plan_stride_dw + L.scratch_dw + L.traf_dw) + my_slot * L.hist_dw;
+  uint32_t* st = lds + L.envs * (L.plan_stride_dw + L.scratch_dw + L.traf_dw + L.hist_dw);
   uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
+  uint8_t* occ = reinterpret_cast<uint8_t*>(traf_w);
+  uint8_t* hist = reinterpret_cast<uint8_t*>(hist_w);
   Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
   uint8_t* q = reinterpret_cast<uint8_t*>(scr_w);
   uint8_t* par = q + c.nt;
 
   EnvView v{};
+  TrafState ts{0, 0, 0, 0};
   int err = 0;
   if (live) {
     v = rec_load(S.rec, i);
+    if ((TR && c.need_car)) {
+      uint4 tr4 = S.traf[i];
+      ts.n_cars = tr4.x & 0xffffu;
+      ts.n_spawners = tr4.x >> 16;
+      ts.next_id = tr4.y;
+      ts.bank = tr4.z;
+    }
     const uint4* src = reinterpret_cast<const uint4*>(S.plan + i * (uint64_t)c.plan_stride);
     for (int k = 0; k < c.plan_stride / 8; k++) {
       uint4 w4 = src[k];
@@ -966,12 +1355,22 @@ __global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, 
     }
   }
   __syncthreads();  // sT ready
+  if (live && (TR && c.need_car)) {
+    // occupancy counters from the current car positions (one coalesced slot row per car index)
+    for (int w = 0; w < c.nt * 8; w++) traf_w[w] = 0u;
+    CarStore cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
+    for (int k = 0; k < (int)ts.n_cars; k++) {
+      uint32_t a = cs.w0[cs.at((int)ts.bank, c.car_cap, k)];
+      int sl = lane_slot(c, pl, (int)(a & 255u), (int)((a >> 8) & 255u));
+      if (sl < 0 || !occ_inc(occ, sl)) err = PGTG_E_UNSUPPORTED;
+    }
+  }
   STAMP(1);
   uint8_t my_sel = 0;
   if (live) {
     if (mode == MODE_STEP) {
       StepResult res{0.0, 0.0};
-      err = env_step(c, S, i, v, pl, actions[i], res);
+      if (!err) err = env_step<TR>(c, S, i, v, pl, actions[i], res, occ, ts, hist);
       const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
       if (out.reward) out.reward[i] = res.reward;
       if (out.cost) out.cost[i] = res.cost;
@@ -993,7 +1392,7 @@ __global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, 
   if (single) {
     if (live && (my_sel != 2)) {
       ObsInfo oi;
-      build_obs(c, S, pl, v, st + tid * L.seg_words, oi);
+      build_obs<TR>(c, S, pl, v, st + tid * L.seg_words, oi, occ);
       write_small_outputs(c, out, i, v, oi, my_sel == 1);
     }
     __syncthreads();
@@ -1001,14 +1400,14 @@ __global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, 
       write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
                 (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel);
   } else if (want_final) {
-    obs_pass(c, S, pl, v, out, out.final_obs, env0, nb, my_sel == 1, true, sel, st, L);
+    obs_pass<TR>(c, S, pl, v, out, out.final_obs, env0, nb, my_sel == 1, true, sel, st, L, occ);
   }
   STAMP(3);
   const bool reset_now = my_sel != 0;
   const int n_resets = __syncthreads_count(reset_now);
   if (tid == 0 && n_resets) atomicAdd(&S.counters[1], (unsigned long long)n_resets);
   if (reset_now) {
-    int e2 = env_reset(c, S, i, v, pl.p, q, par);
+    int e2 = env_reset<TR>(c, S, i, v, pl.p, q, par, occ, ts);
     if (e2) err = e2;
     uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
     for (int k = 0; k < c.plan_stride / 8; k++) {
@@ -1020,14 +1419,17 @@ __global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, 
   }
   STAMP(4);
   if (live) {
-    if (mode != MODE_OBSERVE) rec_store(S.rec, i, v);
+    if (mode != MODE_OBSERVE) {
+      rec_store(S.rec, i, v);
+      if ((TR && c.need_car)) S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.bank, 0u);
+    }
     S.err[i] = (uint8_t)(-err);
   }
   STAMP(5);
   if (single) {
     if (reset_now) {
       ObsInfo oi;
-      build_obs(c, S, pl, v, st + tid * L.seg_words, oi);
+      build_obs<TR>(c, S, pl, v, st + tid * L.seg_words, oi, occ);
       write_small_outputs(c, out, i, v, oi, false);
     }
     __syncthreads();
@@ -1035,7 +1437,7 @@ __global__ void __launch_bounds__(kBlock) k_env(const DevCfg* __restrict__ cfg, 
       write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
                 (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, nullptr);
   } else {
-    obs_pass(c, S, pl, v, out, out.obs, env0, nb, live, false, nullptr, st, L);
+    obs_pass<TR>(c, S, pl, v, out, out.obs, env0, nb, live, false, nullptr, st, L, occ);
   }
   if (mode == MODE_STEP && tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
   STAMP(6);
@@ -1302,8 +1704,37 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
   c.need_broken = kinds[1];
   c.need_sand = kinds[2];
   c.density = in.traffic_density;
-  c.need_car = in.traffic_density > 0;
-  if (c.need_car) return fail(h, PGTG_E_UNSUPPORTED, "traffic is not enabled in this build yet");
+  c.manual_cars = in.min_car_capacity > 0;
+  c.need_car = in.traffic_density > 0 || c.manual_cars;
+  if (c.need_car) {
+    if (c.W > 255 || c.H > 255) return fail(h, PGTG_E_UNSUPPORTED, "traffic needs maps of at most 28x28 tiles");
+    int cap = (int)((double)(c.nt * 32) * in.traffic_density);
+    if (cap < in.min_car_capacity) cap = in.min_car_capacity;
+    if (cap < 1) cap = 1;
+    c.car_cap = cap;
+    c.max_spawners = c.nt * 5;
+    int seen_off = ((2 * cap + 3) / 4) * 4;
+    int pre_off = seen_off + 4 * c.nt;
+    int fl = pre_off + 2 * (c.W + 1);
+    int occ = c.nt * 32;
+    c.floyd_seen_off = seen_off;
+    c.floyd_pre_off = pre_off;
+    c.traf_bytes = ((fl > occ ? fl : occ) + 3) / 4 * 4;
+  }
+  {  // DRIVER_BEHAVIORS (pgtg/environment.py:64-109)
+    const double ys[5] = {0.95, 0.75, 0.3, 0.98, 0.1}, rv[5] = {0.01, 0.05, 0.15, 0.001, 0.3};
+    const int mf[5] = {2, 1, 0, 3, 0};
+    const double pl[5] = {0.9, 0.7, 0.3, 0.95, 0.1}, sm[5] = {0.8, 1.0, 1.3, 0.6, 1.5}, rd[5] = {0.1, 0.15, 0.05, 0.3, 0.1};
+    for (int k = 0; k < 5; k++) {
+      c.beh_yellow[k] = ys[k];
+      c.beh_red[k] = rv[k];
+      c.beh_min_follow[k] = mf[k];
+      c.beh_patience_thr[k] = (int)floor(pl[k] * 10);
+      c.beh_one_minus_patience[k] = 1.0 - pl[k];
+      c.beh_speed[k] = sm[k];
+      c.beh_delay[k] = rd[k];
+    }
+  }
   {
     double tot = 0.0, p[5];
     for (int k = 0; k < 5; k++) tot += in.profile_pct[k];
@@ -1316,7 +1747,13 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
     for (int k = 0; k < 5; k++) c.profile_cdf[k] = cdf[k] / cdf[4];
   }
   c.n_rules = in.n_rules;
-  for (int k = 0; k < in.n_rules && k < PGTG_MAX_RULES; k++) c.rules[k] = in.rules[k];
+  if (in.n_rules < 0 || in.n_rules > PGTG_MAX_RULES) return fail(h, PGTG_E_INVALID, "bad rule count");
+  for (int k = 0; k < in.n_rules; k++) c.rules[k] = in.rules[k];
+  {  // rules that need cars can never fire without traffic: skip the braking pass entirely then
+    bool possible = c.need_car;
+    for (int k = 0; k < in.n_rules; k++) possible = possible || in.rules[k].min_traffic <= 0;
+    if (!possible) c.n_rules = 0;
+  }
   c.nsd_off = c.W > c.H ? c.W : c.H;
   c.nsd_pitch = 2 * c.nsd_off + 1;
   c.cmp_off = c.nsd_off + 2;
@@ -1375,6 +1812,13 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
       ALLOC(streams[k]->buf, n);
     }
   if (c.visited_penalty != 0.0) ALLOC(S.visited, n * (uint64_t)c.vis_words);
+  if (c.need_car) {
+    ALLOC(S.car_w0, 2 * (uint64_t)c.car_cap * n);
+    ALLOC(S.car_w1, 2 * (uint64_t)c.car_cap * n);
+    ALLOC(S.car_id, 2 * (uint64_t)c.car_cap * n);
+    ALLOC(S.traf, n);
+    ALLOC(S.spawners, (uint64_t)c.max_spawners * n);
+  }
   // atan2 tables
   {
     std::vector<int8_t> nsd((size_t)c.nsd_pitch * c.nsd_pitch), cmp((size_t)c.cmp_pitch * c.cmp_pitch);
@@ -1411,6 +1855,28 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     memcpy(t.erev, c.erev, sizeof t.erev);
     memcpy(t.bt, c.bt, sizeof t.bt);
     memcpy(t.bd, c.bd, sizeof t.bd);
+    memset(t.li, 255, sizeof t.li);
+    memset(t.slot_sq, 255, sizeof t.slot_sq);
+    for (int ex = 0; ex < 16; ex++) {
+      int n = 0;
+      for (int lx = 0; lx < 9; lx++)
+        for (int ly = 0; ly < 9; ly++) {
+          int sq = lx * 9 + ly;
+          uint32_t ln = hs::kLanes[ex][sq];
+          if (ln) {
+            t.li[ex][sq] = (uint8_t)n;
+            t.slot_sq[ex][n] = (uint8_t)sq;
+            n++;
+            t.lanecol[ex][lx] |= (uint16_t)(1u << ly);
+          }
+          if ((hs::kLaneSpawner[ex][sq >> 5] >> (sq & 31)) & 1u) t.spcol[ex][lx] |= (uint16_t)(1u << ly);
+          for (int ty = 0; ty < 4; ty++)
+            if ((ln >> (28 + ty)) & 1u) t.allcol[ex][ty][lx] |= (uint16_t)(1u << ly);
+        }
+    }
+    memcpy(t.lane_route, hs::kLaneRoute, sizeof t.lane_route);
+    memcpy(t.route_type_lane, hs::kRouteTypeLane, sizeof t.route_type_lane);
+    for (int r = 0; r < cfg->n_rules && r < PGTG_MAX_RULES; r++) memcpy(t.rule_w[r], cfg->rules[r].weight, sizeof t.rule_w[r]);
     if ((rc = dalloc(h, &h->dtab, 1)) || hipMemcpy(h->dtab, &t, sizeof t, hipMemcpyHostToDevice) != hipSuccess) {
       g_create_err = "table upload failed";
       pgtg_destroy(h);
@@ -1428,6 +1894,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     int envs = n_envs <= (uint64_t)64 * 1024 ? 64 : kBlock;
     if (const char* e = getenv("PGTG_ENVS_PER_BLOCK")) envs = atoi(e);
     if (envs != 64 && envs != 128 && envs != kBlock) envs = kBlock;
+    while (envs > 64 && lds_bytes(lds_layout(c, envs)) + sizeof(Tables) > 150 * 1024) envs /= 2;
     h->L = lds_layout(c, envs);
   }
   h->lds = lds_bytes(h->L);
@@ -1437,7 +1904,10 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     return PGTG_E_UNSUPPORTED;
   }
   if (h->lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)k_env, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+  {
+    (void)hipFuncSetAttribute((const void*)k_env<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+    (void)hipFuncSetAttribute((const void*)k_env<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+  }
   *out = h;
   return PGTG_OK;
 }
@@ -1477,8 +1947,12 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
     }
     HIPCHK(h, hipEventRecord(h->evpool[h->ev_used], h->stream));
   }
-  hipLaunchKernelGGL(k_env, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S, actions,
-                     mask, h->out, mode, h->L);
+  if (h->hcfg.need_car || h->hcfg.n_rules > 0)
+    hipLaunchKernelGGL(k_env<true>, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
+                       actions, mask, h->out, mode, h->L);
+  else
+    hipLaunchKernelGGL(k_env<false>, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
+                       actions, mask, h->out, mode, h->L);
   HIPCHK(h, hipGetLastError());
   if (timed) {
     HIPCHK(h, hipEventRecord(h->evpool[h->ev_used + 1], h->stream));
@@ -1552,11 +2026,35 @@ int pgtg_get_env_state(pgtg_handle* h, uint64_t env, PgtgEnvState* st) {
   return PGTG_OK;
 }
 
+static int read_traf(pgtg_handle* h, uint64_t env, uint4* t) {
+  HIPCHK(h, hipMemcpy(t, h->S.traf + env, sizeof *t, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int pgtg_get_cars(pgtg_handle* h, uint64_t env, PgtgCar* cars, int32_t cap, int32_t* n) {
   if (!h || env >= h->n || !n) return PGTG_E_INVALID;
-  (void)cars;
-  (void)cap;
   *n = 0;
+  if (!h->hcfg.need_car) return PGTG_OK;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  uint4 t;
+  if (int rc = read_traf(h, env, &t)) return rc;
+  int nc = (int)(t.x & 0xffffu), bank = (int)t.z;
+  *n = nc;
+  const uint64_t N = h->n, C = (uint64_t)h->hcfg.car_cap;
+  const int m = nc < cap ? nc : cap;
+  if (cars && m > 0) {
+    // one strided copy per array: slot k of env `env` lives at ((bank*C + k)*N + env)
+    std::vector<uint32_t> w0(m), w1(m), id(m);
+    const uint64_t base = (uint64_t)bank * C * N + env;
+    HIPCHK(h, hipMemcpy2D(w0.data(), 4, h->S.car_w0 + base, N * 4, 4, m, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy2D(w1.data(), 4, h->S.car_w1 + base, N * 4, 4, m, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy2D(id.data(), 4, h->S.car_id + base, N * 4, 4, m, hipMemcpyDeviceToHost));
+    for (int k = 0; k < m; k++)
+      cars[k] = PgtgCar{(int32_t)id[k], (int32_t)(w0[k] & 255u), (int32_t)((w0[k] >> 8) & 255u),
+                        (int32_t)((w0[k] >> 16) & 31u), (int32_t)((w0[k] >> 21) & 7u), (int32_t)w1[k],
+                        (int32_t)((w0[k] >> 24) & 3u)};
+  }
   return PGTG_OK;
 }
 
@@ -1601,9 +2099,25 @@ int pgtg_set_agent(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t v
 }
 
 int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t route, int32_t profile) {
-  if (!h) return PGTG_E_INVALID;
-  (void)env; (void)x; (void)y; (void)route; (void)profile;
-  return fail(h, PGTG_E_UNSUPPORTED, "traffic is not enabled in this build yet");
+  if (!h || env >= h->n) return PGTG_E_INVALID;
+  if (!h->hcfg.need_car) return fail(h, PGTG_E_UNSUPPORTED, "create the handle with min_car_capacity > 0 or traffic");
+  if (x < 0 || y < 0 || x >= h->hcfg.W || y >= h->hcfg.H || route < 0 || route >= 20 || profile < 0 || profile >= 5)
+    return fail(h, PGTG_E_INVALID, "car outside the map or bad route/profile");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  uint4 t;
+  if (int rc = read_traf(h, env, &t)) return rc;
+  int nc = (int)(t.x & 0xffffu), bank = (int)t.z;
+  if (nc >= h->hcfg.car_cap) return fail(h, PGTG_E_UNSUPPORTED, "car capacity exhausted");
+  const uint64_t a = ((uint64_t)bank * h->hcfg.car_cap + nc) * h->n + env;
+  uint32_t w0 = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)profile << 21, w1 = 0, id = t.y;
+  HIPCHK(h, hipMemcpy(h->S.car_w0 + a, &w0, 4, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->S.car_w1 + a, &w1, 4, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->S.car_id + a, &id, 4, hipMemcpyHostToDevice));
+  t.x = (t.x & 0xffff0000u) | (uint32_t)(nc + 1);
+  t.y += 1;
+  HIPCHK(h, hipMemcpy(h->S.traf + env, &t, sizeof t, hipMemcpyHostToDevice));
+  return PGTG_OK;
 }
 
 int pgtg_get_counters(pgtg_handle* h, uint64_t* env_steps, uint64_t* episodes) {

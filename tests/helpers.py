@@ -121,6 +121,8 @@ def replay_vec(d: dict, n_envs: int | None = None, steps: int | None = None) -> 
     m = env.obs_map.cpu().numpy()[:, perm]
     pos = env.position.cpu().numpy()
     for i in range(N):
+        if has_traffic(meta) and digest(env.cars(i)) != int(d["init_cars_dig"][i]):
+            bad.append(f"env{i} reset cars")
         if not np.array_equal(m[i], d["init_obs"][i]):
             bad.append(f"env{i} reset obs")
         if tuple(pos[i]) != tuple(d["init_pos"][i]):
@@ -141,8 +143,14 @@ def replay_vec(d: dict, n_envs: int | None = None, steps: int | None = None) -> 
         cost = env.cost.cpu().numpy() if env.cost is not None else np.zeros(N)
         nsd = env.nsd.cpu().numpy() if env.nsd is not None else None
         fnsd = env.final_nsd.cpu().numpy() if env.final_nsd is not None else None
+        check_cars = has_traffic(meta)
         for i in range(N):
             tag = f"env{i} t{t}"
+            if check_cars:
+                dig = digest(env.cars(i))
+                want = d["reset_cars_dig"][reset_map[(t, i)]] if term[i] else d["cars_dig"][t, i]
+                if dig != int(want):
+                    bad.append(f"{tag} cars")
             if bool(term[i]) != bool(d["terminated"][t, i]) or trunc[i]:
                 bad.append(f"{tag} terminated {term[i]} vs {d['terminated'][t, i]}")
                 continue

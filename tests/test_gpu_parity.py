@@ -6,10 +6,7 @@ import helpers
 
 pytestmark = pytest.mark.gpu
 
-NO_TRAFFIC = [n for n in helpers.traj_names() if not helpers.has_traffic(helpers.load_traj(n)["meta"])]
-
-
-@pytest.mark.parametrize("name", NO_TRAFFIC)
+@pytest.mark.parametrize("name", helpers.traj_names())
 def test_golden_trajectory(name):
     d = helpers.load_traj(name)
     bad = helpers.replay_vec(d)
