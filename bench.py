@@ -32,10 +32,12 @@ WORKLOADS = {
              262144, dict(random_map_width=3, random_map_height=3)),
     "cfg5": (4, "5x5 map, 131072 envs per GPU (1048576 over 8 GPUs), random actions, auto-reset",
              131072, dict(random_map_width=5, random_map_height=5)),
+    "cfg3": (2, "65536 envs, 5x5 procedural map, traffic density 0.5, random actions, auto-reset",
+             65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5)),
 }
 
 
-def algorithmic_bytes(spec, n_envs: int, resets: float) -> float:
+def algorithmic_bytes(spec, n_envs: int, resets: float, cars_per_env: float = 0.0) -> float:
     """Bytes one step launch must move (DESIGN.md "Algorithmic bytes"): per env-step the action,
     the 32-B agent record read+written, the 2-B/tile plan read, the observation and small outputs
     written; per reset the seed read, the new plan written and the terminal observation written."""
@@ -44,6 +46,11 @@ def algorithmic_bytes(spec, n_envs: int, resets: float) -> float:
     small = 8 + 8 + 8 + 3 + (4 if spec.next_subgoal else 0) + (8 if spec.separate_reward_cost else 0)
     per_step = 1 + 2 * 32 + 2 * nt + obs + small
     per_reset = 8 + 2 * nt + obs + 16 + (4 if spec.next_subgoal else 0)
+    if cars_per_env:
+        # cars: 12 B per car read + written per step, car_rng state 80 B r/w, traffic record 16 B r/w;
+        # resets write the new cars (12 B each) and the spawner list (2 B per spawner, ~nt)
+        per_step += 2 * 12 * cars_per_env + 2 * 40 + 2 * 16
+        per_reset += 12 * cars_per_env + 2 * nt + 80
     return n_envs * per_step + resets * per_reset
 
 
@@ -140,7 +147,8 @@ def main():
     if rank == 0:
         resets_per_launch = (eps1 - eps0) / max(1, args.steps)
         avg_kernel_s = (kern_ms / max(1, launches)) / 1e3
-        alg = algorithmic_bytes(spec, n_local, resets_per_launch)
+        cars = env.mean_cars() if spec.traffic_density > 0 else 0.0
+        alg = algorithmic_bytes(spec, n_local, resets_per_launch, cars)
         achieved = alg / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
         rec = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -155,7 +163,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": load_traffic(args.workload, alg),
                          "kernel": "pgtg::k_env (step + auto-reset)", "avg_kernel_us": avg_kernel_s * 1e6,
-                         "alg_bytes_per_launch": alg, "resets_per_launch": resets_per_launch},
+                         "alg_bytes_per_launch": alg, "resets_per_launch": resets_per_launch,
+                         "envs_per_workgroup": env.launch_info()[0], "lds_bytes": env.launch_info()[1]},
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)

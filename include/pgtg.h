@@ -171,6 +171,8 @@ int pgtg_get_counters(pgtg_handle* h, uint64_t* env_steps, uint64_t* episodes);
 int pgtg_error_count(pgtg_handle* h, uint64_t* n_errors, int32_t* first_code);
 int pgtg_window(const pgtg_handle* h);
 uint64_t pgtg_num_envs(const pgtg_handle* h);
+/* Launch geometry of the step kernel: envs per 256-lane workgroup and dynamic LDS bytes. */
+int pgtg_launch_info(const pgtg_handle* h, int32_t* envs_per_block, int32_t* lds_bytes);
 const char* pgtg_last_error(const pgtg_handle* h);
 /* Per-launch device timing of the step kernel with HIP events on the handle's stream.  When enabled,
  * every pgtg_step brackets its kernel with an event pair; pgtg_timing_read synchronises and returns

@@ -55,7 +55,7 @@ struct DevCfg {
   int32_t n_border, n_border_add;
   uint8_t bt[kMaxBorder], bd[kMaxBorder];
   double obstacle_probability;
-  double obst_cdf[4];
+  uint64_t obst_cdf_t[4];  // obstacle-type CDF as 53-bit thresholds
   double ice_p, broken_p, sand_p;
   int32_t phase_total, phase_g, phase_gy;
   int32_t ignore_collisions, separate_cost, autoreset, max_steps;
@@ -65,14 +65,16 @@ struct DevCfg {
   int32_t channels[PGTG_MAX_CHANNELS];
   int32_t need_car, need_ice, need_broken, need_sand;
   double density;
-  double profile_cdf[5];
+  uint64_t profile_t[5];  // profile CDF as 53-bit thresholds: random() < cdf[j]  <=>  (next64 >> 11) < t[j]
   int32_t car_cap;      // car slots per env and bank
   int32_t max_spawners; // spawner list capacity per env (nt * 5)
   // DRIVER_BEHAVIORS (pgtg/environment.py:64-109) in DriverProfile order, thresholds precomputed
-  double beh_yellow[5], beh_red[5], beh_one_minus_patience[5], beh_speed[5], beh_delay[5];
+  // random() < p  <=>  (next64 >> 11) < ceil(p * 2^53): probabilities as integer thresholds
+  uint64_t beh_t[5][5];  // [BEH_*][profile]
   int32_t beh_min_follow[5], beh_patience_thr[5];  // patience > level*10  <=>  patience > floor(level*10)
   int32_t traf_bytes;      // per-lane LDS traffic region (occupancy counters / reset scratch)
-  int32_t floyd_seen_off;  // byte offsets inside it used during traffic_reset
+  int32_t floyd_out_off;   // byte offsets inside it used during traffic_reset
+  int32_t floyd_seen_off;
   int32_t floyd_pre_off;
   int32_t manual_cars;     // cars may be added through pgtg_add_car
   int32_t n_rules;
@@ -106,6 +108,10 @@ struct Tables {
   uint8_t lane_route[32];
   uint8_t route_type_lane[20][4];
   uint8_t rule_w[PGTG_MAX_RULES][6][20];
+  // DRIVER_BEHAVIORS per profile, read per car by profile index (kept in LDS, not in the DevCfg
+  // constant block, so a per-lane index never becomes a dependent global load)
+  uint64_t beh_t[5][5];    // [BEH_*][profile] 53-bit thresholds
+  int32_t beh_mf[5], beh_pt[5];  // min_following_distance, floor(patience_level * 10)
 };
 
 // one PCG64 stream, SoA over envs
@@ -116,6 +122,8 @@ struct DevStream {
   uint64_t* ilo;
   uint64_t* buf;  // bit 32 = has_uint32, low 32 = buffered value
 };
+
+enum { BEH_DELAY = 0, BEH_SPEED = 1, BEH_YELLOW = 2, BEH_RED = 3, BEH_GO = 4 };
 
 struct DevState {
   uint64_t n;
@@ -173,6 +181,7 @@ __device__ __forceinline__ uint32_t pcg_next32(Pcg& g) {
   g.buf = (uint32_t)(v >> 32);
   return (uint32_t)v;
 }
+__device__ __forceinline__ uint64_t pcg_u53(Pcg& g) { return pcg_next64(g) >> 11; }
 __device__ __forceinline__ double pcg_double(Pcg& g) {
   return (double)(pcg_next64(g) >> 11) * (1.0 / 9007199254740992.0);
 }
@@ -192,15 +201,25 @@ __device__ __forceinline__ uint32_t pcg_int(Pcg& g, uint32_t n) {
   }
   return (uint32_t)(m >> 32);
 }
-// choice(k, p=p) with the host-normalised CDF (cumsum(p)/cumsum[-1]): searchsorted(u, 'right')
+// choice(k, p=p) with the host-normalised CDF (cumsum(p)/cumsum[-1]) as 53-bit thresholds:
+// searchsorted(u, 'right') counts the entries <= u
 template <int K>
-__device__ __forceinline__ int pcg_choice_cdf(Pcg& g, const double* cdf) {
-  double u = pcg_double(g);
+__device__ __forceinline__ int pcg_choice_cdf(Pcg& g, const uint64_t* cdf_t) {
+  const uint64_t m = pcg_u53(g);
   int i = 0;
 #pragma unroll
-  for (int j = 0; j < K - 1; j++) i += (u < cdf[j]) ? 0 : 1;
-  // cdf is non-decreasing: i counts entries <= u, clamp for safety
-  return i < K ? i : K - 1;
+  for (int j = 0; j < K - 1; j++) i += (m < cdf_t[j]) ? 0 : 1;
+  return i;
+}
+// per-lane pick of a uniform 5-entry row (selects over scalar values instead of an indexed load)
+template <typename T>
+__device__ __forceinline__ T pick5(const T* a, int k) {
+  T r = a[0];
+  r = k == 1 ? a[1] : r;
+  r = k == 2 ? a[2] : r;
+  r = k == 3 ? a[3] : r;
+  r = k == 4 ? a[4] : r;
+  return r;
 }
 
 __device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t& hc) {

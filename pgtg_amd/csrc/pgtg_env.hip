@@ -43,12 +43,12 @@ __shared__ Tables sT;  // per-workgroup LDS copy of the lane-indexed tables
 // Diagnostic build only (-DPGTG_STAMPS): per-wave phase timestamps (s_memtime) into a debug buffer
 // that nothing else reads.  The product build compiles these to nothing.
 #ifdef PGTG_STAMPS
-__device__ unsigned long long g_stamps[1 << 20];
+__device__ unsigned long long g_stamps[1 << 21];
 #define STAMP(k)                                                                          \
   do {                                                                                    \
     if ((threadIdx.x & 63) == 0) {                                                        \
       unsigned long long t_ = __builtin_amdgcn_s_memtime();                               \
-      g_stamps[((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16 + (k)) & ((1 << 20) - 1)] = t_; \
+      g_stamps[((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 32 + (k)) & ((1 << 21) - 1)] = t_; \
     }                                                                                     \
   } while (0)
 #else
@@ -409,7 +409,7 @@ __device__ __forceinline__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* 
       uint32_t e = plan[t];
       double u = pcg_double(r);
       if (u < c.obstacle_probability && e != 0u) {
-        int ot = pcg_choice_cdf<4>(r, c.obst_cdf);
+        int ot = pcg_choice_cdf<4>(r, c.obst_cdf_t);
         uint32_t om;
         if (ot != 3) {
           om = pcg_int(r, 8);
@@ -486,11 +486,12 @@ __device__ __forceinline__ uint32_t spawner_colmask(const DevCfg& c, uint32_t ex
 
 // Initial traffic of a fresh episode (EpisodeMap scans pgtg/map.py:31-42 and
 // _create_initial_traffic pgtg/environment.py:830-879).  `tr` is the lane's LDS traffic region:
-// Floyd's output/seen set and the column prefix alias the occupancy counters, which are rebuilt
-// from the new cars at the end.
+// layout: occupancy counters [0, nt*32), then Floyd's output, its seen set and the column prefix,
+// so the counters are built while the cars are created.
 __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S, uint64_t i, const Plan& pl,
                                              Pcg& cr, uint8_t* tr, TrafState& ts) {
   const uint64_t N = S.n;
+  STAMP(19);
   // car spawners in x-major order -> HBM list
   int nsp = 0;
   for (int x = 0; x < c.W; x++) {
@@ -520,12 +521,14 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
   const int ncars = (int)((double)np * c.density);  // int(len(positions) * traffic_density)
   int k = 0;
   CarStore cs{S.car_w0, S.car_w1, S.car_id, N, i};
+  for (int w = 0; w < c.nt * 8; w++) reinterpret_cast<uint32_t*>(tr)[w] = 0u;
   if (ncars > 0 && np > 0) {
     k = min(ncars, np);
     if (k > c.car_cap) return PGTG_E_UNSUPPORTED;
-    uint16_t* out = reinterpret_cast<uint16_t*>(tr);
+    uint16_t* out = reinterpret_cast<uint16_t*>(tr + c.floyd_out_off);
     uint32_t* seen = reinterpret_cast<uint32_t*>(tr + c.floyd_seen_off);
     for (int w = 0; w < (np + 31) / 32; w++) seen[w] = 0u;
+    STAMP(20);
     // Generator.choice(np, k, replace=False): Floyd's algorithm, then _shuffle_int
     for (int j = np - k; j < np; j++) {
       int val = (int)pcg_int(cr, (uint32_t)(j + 1));
@@ -533,12 +536,14 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
       seen[val >> 5] |= 1u << (val & 31);
       out[j - (np - k)] = (uint16_t)val;
     }
+    STAMP(21);
     for (int m = k - 1; m >= 1; m--) {
       int jj = (int)pcg_int(cr, (uint32_t)(m + 1));
       uint16_t t = out[m];
       out[m] = out[jj];
       out[jj] = t;
     }
+    STAMP(22);
     for (int m = 0; m < k; m++) {
       int idx = out[m];
       // x: last column whose prefix <= idx
@@ -561,25 +566,21 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
       uint32_t rl = square_lanes(c, pl, x, y) & 0x0fffffffu;
       int nr = __popc(rl);
       if (nr == 0) return PGTG_E_MAP;  // "a car was spawned on a field where no car lane was found"
-      int prof = pcg_choice_cdf<5>(cr, c.profile_cdf);
+      int prof = pcg_choice_cdf<5>(cr, c.profile_t);
       int route = sT.lane_route[kth_bit(rl, (int)pcg_int(cr, (uint32_t)nr))];
       uint64_t a = cs.at(0, c.car_cap, m);
       cs.w0[a] = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
       cs.w1[a] = 0u;
       cs.id[a] = (uint32_t)m;
+      const int sl = lane_slot(c, pl, x, y);
+      if (sl < 0 || !occ_inc(tr, sl)) return PGTG_E_UNSUPPORTED;
     }
   }
+  STAMP(23);
   ts.n_cars = (uint32_t)k;
   ts.n_spawners = (uint32_t)min(nsp, c.max_spawners);
   ts.next_id = (uint32_t)k;
   ts.bank = 0;
-  // occupancy counters of the new cars
-  for (int w = 0; w < c.nt * 8; w++) reinterpret_cast<uint32_t*>(tr)[w] = 0u;
-  for (int m = 0; m < k; m++) {
-    uint32_t a = cs.w0[cs.at(0, c.car_cap, m)];
-    int sl = lane_slot(c, pl, (int)(a & 255u), (int)((a >> 8) & 255u));
-    if (sl < 0 || !occ_inc(tr, sl)) return PGTG_E_UNSUPPORTED;
-  }
   return 0;
 }
 
@@ -848,21 +849,41 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
 __device__ __forceinline__ int acc_x(int a) { return a / 3 - 1; }
 __device__ __forceinline__ int acc_y(int a) { return a % 3 - 1; }
 
+struct BrakeQuery {
+  uint32_t cand;  // rules whose tile/speed conditions hold
+  int tile;       // agent tile (-1: nothing to count)
+  int s2;         // squared speed after the acceleration
+  int n_in;       // cars in the tile after the move
+};
 // Traffic tick: every car of the tick-start list, in list order (pgtg/environment.py:1121-1127,
 // _get_next_car_position_and_route :881-968, _should_car_move :678-691, traffic lights :664-676,
 // _spawn_new_car :970-1002).  Survivors go to the other bank in order, respawned cars are appended
 // after them in creation order; occupancy counters follow every move so later cars see earlier ones.
 __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uint64_t i, const EnvView& v,
-                                         const Plan& pl, uint8_t* occ, TrafState& ts, Pcg& cr, int color) {
+                                         const Plan& pl, uint8_t* occ, const uint16_t* sp, TrafState& ts, Pcg& cr,
+                                         int color, BrakeQuery& bq, uint8_t* hist) {
   CarStore cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
   const int cap = c.car_cap, cur = (int)ts.bank, nxt = cur ^ 1;
   const int n0 = (int)ts.n_cars;
   int w = 0, nnew = 0;
+  // software pipeline: the next car's words are requested before the current car is processed, so
+  // their HBM latency overlaps this car's work (the loop-carried copy waits only at the iteration end)
+  uint32_t na, npat, nid;
+  {
+    const uint64_t ar = cs.at(cur, cap, 0);
+    na = cs.w0[ar];
+    npat = cs.w1[ar];
+    nid = cs.id[ar];
+  }
   for (int r = 0; r < n0; r++) {
-    const uint64_t ar = cs.at(cur, cap, r);
-    const uint32_t a = cs.w0[ar];
-    uint32_t pat = cs.w1[ar];
-    const uint32_t id = cs.id[ar];
+    const uint32_t a = na, id = nid;
+    uint32_t pat = npat;
+    {
+      const uint64_t ar = cs.at(cur, cap, r + 1 < n0 ? r + 1 : r);
+      na = cs.w0[ar];
+      npat = cs.w1[ar];
+      nid = cs.id[ar];
+    }
     const int x = (int)(a & 255u), y = (int)((a >> 8) & 255u), prof = (int)((a >> 21) & 7u);
     int route = (int)((a >> 16) & 31u), delay = (int)((a >> 24) & 3u);
     int nx = x, ny = y;
@@ -871,11 +892,11 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
     if (delay > 0) {
       delay -= 1;
       move = false;
-    } else if (pcg_double(cr) < c.beh_delay[prof]) {
+    } else if (pcg_u53(cr) < sT.beh_t[BEH_DELAY][prof]) {
       delay = 1 + (int)pcg_int(cr, 3);  // integers(1, 4)
       move = false;
     } else {
-      move = pcg_double(cr) < c.beh_speed[prof];
+      move = pcg_u53(cr) < sT.beh_t[BEH_SPEED][prof];
     }
     if (!move) {
       pat += 1;
@@ -900,15 +921,15 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
             decided = true;
             bool stop = false;
             if (square_tlight(c, pl, px, py)) {
-              if (color == 1) stop = pcg_double(cr) < c.beh_yellow[prof];
-              else if (color == 2) stop = pcg_double(cr) >= c.beh_red[prof];
+              if (color == 1) stop = pcg_u53(cr) < sT.beh_t[BEH_YELLOW][prof];
+              else if (color == 2) stop = !(pcg_u53(cr) < sT.beh_t[BEH_RED][prof]);
             }
             if (stop) {
               pat += 1;
             } else if (occ_at(c, pl, occ, px, py) > 0) {
               bool go = false;
-              if (c.beh_min_follow[prof] == 0 || (int)pat > c.beh_patience_thr[prof])
-                go = pcg_double(cr) < c.beh_one_minus_patience[prof];
+              if (sT.beh_mf[prof] == 0 || (int)pat > sT.beh_pt[prof])
+                go = pcg_u53(cr) < sT.beh_t[BEH_GO][prof];
               if (go) {
                 pat = 0;
                 nx = px;
@@ -935,13 +956,13 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       // _spawn_new_car: choice(car_spawners) -> sorted routes -> profile -> route
       int sx = 0, sy = 0;
       if (ts.n_spawners > 0) {
-        uint32_t code = S.spawners[(uint64_t)pcg_int(cr, ts.n_spawners) * S.n + i];
+        uint32_t code = sp[pcg_int(cr, ts.n_spawners)];
         sx = (int)(code & 255u);
         sy = (int)(code >> 8);
       }
       const uint32_t rl = square_lanes(c, pl, sx, sy) & 0x0fffffffu;
       const int nr = __popc(rl);
-      const int nprof = pcg_choice_cdf<5>(cr, c.profile_cdf);
+      const int nprof = pcg_choice_cdf<5>(cr, c.profile_t);
       if (nr == 0) return PGTG_E_MAP;
       const int nroute = sT.lane_route[kth_bit(rl, (int)pcg_int(cr, (uint32_t)nr))];
       const uint64_t an = cs.at(nxt, cap, n0 - 1 - nnew);
@@ -951,10 +972,20 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       nnew++;
       const int s_new = lane_slot(c, pl, sx, sy);
       if (s_new < 0 || !occ_inc(occ, s_new)) return PGTG_E_UNSUPPORTED;
+      if (bq.tile >= 0 && (s_new >> 5) == bq.tile) {
+        bq.n_in++;
+        hist[nroute]++;
+      }
     } else {
+      int s_cur = s_old;
       if (nx != x || ny != y) {
         occ[s_old]--;
-        if (!occ_inc(occ, lane_slot(c, pl, nx, ny))) return PGTG_E_UNSUPPORTED;
+        s_cur = lane_slot(c, pl, nx, ny);
+        if (!occ_inc(occ, s_cur)) return PGTG_E_UNSUPPORTED;
+      }
+      if (bq.tile >= 0 && (s_cur >> 5) == bq.tile) {
+        bq.n_in++;
+        hist[route]++;
       }
       const uint64_t aw = cs.at(nxt, cap, w);
       cs.w0[aw] = (uint32_t)nx | (uint32_t)ny << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21 | (uint32_t)delay << 24;
@@ -979,30 +1010,23 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
 }
 
 // TrafficRuleEngine.apply_braking (pgtg/environment.py:226-294) on the agent's (clamped) tile after
-// the cars moved; returns true if any rule triggers.  hist: per-lane LDS route histogram (20 B).
-__device__ __forceinline__ bool apply_braking(const DevCfg& c, const DevState& S, uint64_t i, const EnvView& v,
-                                              const Plan& pl, const TrafState& ts, uint8_t* hist) {
+// the cars moved.  Split in two: the rules that can fire for the tile and the new speed are found
+// before the car pass, which then counts the cars ending in that tile into `hist` (per-lane LDS
+// route histogram, 20 B), so the braking test needs no extra pass over the car list.
+__device__ __forceinline__ BrakeQuery braking_query(const DevCfg& c, const EnvView& v, const Plan& pl, int vx, int vy) {
+  BrakeQuery q{0u, -1, vx * vx + vy * vy, 0};
   const int tx = min(max((int)floorf((float)v.px / kTile), 0), c.tw - 1);
   const int ty = min(max((int)floorf((float)v.py / kTile), 0), c.th - 1);
   const uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
-  const int s2 = v.vx * v.vx + v.vy * v.vy;
-  uint32_t cand = 0;
   for (int r = 0; r < c.n_rules; r++)
-    if (c.rules[r].tile_exits == (int)ex && s2 >= c.rules[r].speed_sq_min && s2 <= c.rules[r].speed_sq_max)
-      cand |= 1u << r;
-  if (!cand) return false;
-  // traffic in the tile: count + route histogram
-  CarStore cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
-  for (int r = 0; r < 20; r++) hist[r] = 0;
-  int n_in = 0;
-  for (int k = 0; k < (int)ts.n_cars; k++) {
-    uint32_t a = cs.w0[cs.at((int)ts.bank, c.car_cap, k)];
-    int x = (int)(a & 255u), y = (int)((a >> 8) & 255u);
-    if (x / kTile == tx && y / kTile == ty) {
-      n_in++;
-      hist[(a >> 16) & 31u]++;
-    }
-  }
+    if (c.rules[r].tile_exits == (int)ex && q.s2 >= c.rules[r].speed_sq_min && q.s2 <= c.rules[r].speed_sq_max)
+      q.cand |= 1u << r;
+  if (q.cand) q.tile = ty * c.tw + tx;
+  return q;
+}
+__device__ __forceinline__ bool braking_decide(const DevCfg& c, const DevState& S, const EnvView& v, const Plan& pl,
+                                               const BrakeQuery& q, const uint8_t* hist) {
+  if (!q.cand) return false;
   // agent direction from the subgoal compass (environment.py:185-206, 1037-1090)
   int dir;
   int bx = 0, by = 0;
@@ -1010,12 +1034,12 @@ __device__ __forceinline__ bool apply_braking(const DevCfg& c, const DevState& S
   if (nearest_goal_square(c, pl, v, v.px, v.py, bx, by))
     cp = S.cmp_tab[(bx - v.px + c.cmp_off) * c.cmp_pitch + (by - v.py + c.cmp_off)];
   if (cp >= 0) dir = cp >> 1;  // N,NE -> south_to_north; E,SE -> west_to_east; S,SW; W,NW
-  else dir = s2 == 0 ? 4 : 5;  // "stationary" (speed < 0.1) / "near_goal"
+  else dir = q.s2 == 0 ? 4 : 5;  // "stationary" (speed < 0.1) / "near_goal"
   for (int r = 0; r < c.n_rules; r++) {
-    if (!((cand >> r) & 1u)) continue;
-    if (n_in < c.rules[r].min_traffic) continue;
+    if (!((q.cand >> r) & 1u)) continue;
+    if (q.n_in < c.rules[r].min_traffic) continue;
     int match = 0;
-    for (int q = 0; q < 20; q++) match += hist[q] * (int)sT.rule_w[r][dir][q];
+    for (int k = 0; k < 20; k++) match += hist[k] * (int)sT.rule_w[r][dir][k];
     if (match >= c.rules[r].min_matching_traffic) return true;
   }
   return false;
@@ -1027,17 +1051,26 @@ struct StepResult {
 
 template <bool TR>
 __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, const Plan& pl,
-                                        int action, StepResult& res, uint8_t* occ, TrafState& ts, uint8_t* hist) {
+                                        int action, StepResult& res, uint8_t* occ, const uint16_t* sp, TrafState& ts,
+                                        uint8_t* hist) {
   res.reward = 0.0;
   res.cost = 0.0;
   if (v.flags & (kFlagTerminated | kFlagTruncated)) return PGTG_E_DONE;
   if ((unsigned)action > 8u) return PGTG_E_INVALID;
   v.phase = (v.phase + 1u) % (uint32_t)c.phase_total;
   const int ax = acc_x(action), ay = acc_y(action);
+  BrakeQuery bq{0u, -1, 0, 0};
+  if (TR && c.n_rules > 0) {
+    bq = braking_query(c, v, pl, v.vx + ax, v.vy + ay);
+    if (bq.cand)
+      for (int k = 0; k < 20; k++) hist[k] = 0;
+  }
   // cars move first (environment.py:1120-1127), with this tick's light phase
   if ((TR && c.need_car) && ts.n_cars > 0) {
     Pcg cr = stream_load(S.car, i);
-    int e = move_cars(c, S, i, v, pl, occ, ts, cr, phase_color(c, v.phase));
+    STAMP(16);
+    int e = move_cars(c, S, i, v, pl, occ, sp, ts, cr, phase_color(c, v.phase), bq, hist);
+    STAMP(17);
     stream_store_state(S.car, i, cr);
     if (e) return e;
   }
@@ -1046,10 +1079,11 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
   v.vx += ax;
   v.vy += ay;
   v.flags &= ~kFlagBraking;
-  if (TR && c.n_rules > 0 && apply_braking(c, S, i, v, pl, ts, hist)) {  // environment.py:1145
+  if (TR && c.n_rules > 0 && braking_decide(c, S, v, pl, bq, hist)) {  // environment.py:1145
     v.vx = v.vy = 0;
     v.flags |= kFlagBraking;
   }
+  STAMP(18);
   if (abs(v.vx) > 30000 || abs(v.vy) > 30000) return PGTG_E_UNSUPPORTED;
   Pcg ice, broken, sand;
   if (c.need_ice) ice = stream_load(S.ice, i);
@@ -1328,6 +1362,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   uint32_t* st = lds + L.envs * (L.plan_stride_dw + L.scratch_dw + L.traf_dw + L.hist_dw);
   uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
   uint8_t* occ = reinterpret_cast<uint8_t*>(traf_w);
+  uint16_t* sp_l = reinterpret_cast<uint16_t*>(occ + c.floyd_out_off);  // spawner list during the step
   uint8_t* hist = reinterpret_cast<uint8_t*>(hist_w);
   Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
   uint8_t* q = reinterpret_cast<uint8_t*>(scr_w);
@@ -1359,10 +1394,28 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     // occupancy counters from the current car positions (one coalesced slot row per car index)
     for (int w = 0; w < c.nt * 8; w++) traf_w[w] = 0u;
     CarStore cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
-    for (int k = 0; k < (int)ts.n_cars; k++) {
-      uint32_t a = cs.w0[cs.at((int)ts.bank, c.car_cap, k)];
-      int sl = lane_slot(c, pl, (int)(a & 255u), (int)((a >> 8) & 255u));
-      if (sl < 0 || !occ_inc(occ, sl)) err = PGTG_E_UNSUPPORTED;
+    const int nc = (int)ts.n_cars;
+    for (int k0 = 0; k0 < nc; k0 += 16) {  // 16 independent loads in flight per lane
+      uint32_t a16[16];
+#pragma unroll
+      for (int g = 0; g < 16; g++) a16[g] = cs.w0[cs.at((int)ts.bank, c.car_cap, k0 + g < nc ? k0 + g : 0)];
+#pragma unroll
+      for (int g = 0; g < 16; g++) {
+        if (k0 + g < nc) {
+          int sl = lane_slot(c, pl, (int)(a16[g] & 255u), (int)((a16[g] >> 8) & 255u));
+          if (sl < 0 || !occ_inc(occ, sl)) err = PGTG_E_UNSUPPORTED;
+        }
+      }
+    }
+    // the spawner list (respawn positions) into the reset-scratch part of the traffic region
+    const int nsp = (int)ts.n_spawners;
+    for (int k0 = 0; k0 < nsp; k0 += 8) {
+      uint16_t s8[8];
+#pragma unroll
+      for (int g = 0; g < 8; g++) s8[g] = S.spawners[(uint64_t)(k0 + g < nsp ? k0 + g : 0) * S.n + i];
+#pragma unroll
+      for (int g = 0; g < 8; g++)
+        if (k0 + g < nsp) sp_l[k0 + g] = s8[g];
     }
   }
   STAMP(1);
@@ -1370,7 +1423,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (live) {
     if (mode == MODE_STEP) {
       StepResult res{0.0, 0.0};
-      if (!err) err = env_step<TR>(c, S, i, v, pl, actions[i], res, occ, ts, hist);
+      if (!err) err = env_step<TR>(c, S, i, v, pl, actions[i], res, occ, sp_l, ts, hist);
       const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
       if (out.reward) out.reward[i] = res.reward;
       if (out.cost) out.cost[i] = res.cost;
@@ -1552,6 +1605,14 @@ static int8_t compass_dir(int dx, int dy, int s) {  // environment.py:1058-1090
   return -1;
 }
 
+// random() < p  <=>  m < p * 2^53 for the 53-bit integer m  <=>  m < ceil(p * 2^53) (exact: scaling by
+// a power of two is exact in binary64)
+static uint64_t u53_threshold(double p) {
+  if (!(p > 0.0)) return 0;
+  if (p >= 1.0) return 1ull << 53;
+  return (uint64_t)ceil(ldexp(p, 53));
+}
+
 static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
   memset(&c, 0, sizeof c);
   if (in.abi_version != PGTG_ABI_VERSION) return fail(h, PGTG_E_INVALID, "ABI version mismatch");
@@ -1657,7 +1718,7 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
       acc += p[k];
       cdf[k] = acc;
     }
-    for (int k = 0; k < 4; k++) c.obst_cdf[k] = cdf[k] / cdf[3];
+    for (int k = 0; k < 4; k++) c.obst_cdf_t[k] = u53_threshold(cdf[k] / cdf[3]);
   }
   c.ice_p = in.ice_probability;
   c.broken_p = in.street_damage_probability;
@@ -1713,26 +1774,27 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
     if (cap < 1) cap = 1;
     c.car_cap = cap;
     c.max_spawners = c.nt * 5;
-    int seen_off = ((2 * cap + 3) / 4) * 4;
+    int out_off = c.nt * 32;  // occupancy counters first
+    const int out_n = cap > c.max_spawners ? cap : c.max_spawners;  // Floyd output / spawner list
+    int seen_off = out_off + ((2 * out_n + 3) / 4) * 4;
     int pre_off = seen_off + 4 * c.nt;
-    int fl = pre_off + 2 * (c.W + 1);
-    int occ = c.nt * 32;
+    c.floyd_out_off = out_off;
     c.floyd_seen_off = seen_off;
     c.floyd_pre_off = pre_off;
-    c.traf_bytes = ((fl > occ ? fl : occ) + 3) / 4 * 4;
+    c.traf_bytes = (pre_off + 2 * (c.W + 1) + 3) / 4 * 4;
   }
   {  // DRIVER_BEHAVIORS (pgtg/environment.py:64-109)
     const double ys[5] = {0.95, 0.75, 0.3, 0.98, 0.1}, rv[5] = {0.01, 0.05, 0.15, 0.001, 0.3};
     const int mf[5] = {2, 1, 0, 3, 0};
     const double pl[5] = {0.9, 0.7, 0.3, 0.95, 0.1}, sm[5] = {0.8, 1.0, 1.3, 0.6, 1.5}, rd[5] = {0.1, 0.15, 0.05, 0.3, 0.1};
     for (int k = 0; k < 5; k++) {
-      c.beh_yellow[k] = ys[k];
-      c.beh_red[k] = rv[k];
+      c.beh_t[BEH_YELLOW][k] = u53_threshold(ys[k]);
+      c.beh_t[BEH_RED][k] = u53_threshold(rv[k]);
       c.beh_min_follow[k] = mf[k];
       c.beh_patience_thr[k] = (int)floor(pl[k] * 10);
-      c.beh_one_minus_patience[k] = 1.0 - pl[k];
-      c.beh_speed[k] = sm[k];
-      c.beh_delay[k] = rd[k];
+      c.beh_t[BEH_GO][k] = u53_threshold(1.0 - pl[k]);
+      c.beh_t[BEH_SPEED][k] = u53_threshold(sm[k]);
+      c.beh_t[BEH_DELAY][k] = u53_threshold(rd[k]);
     }
   }
   {
@@ -1744,7 +1806,7 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
       acc += p[k];
       cdf[k] = acc;
     }
-    for (int k = 0; k < 5; k++) c.profile_cdf[k] = cdf[k] / cdf[4];
+    for (int k = 0; k < 5; k++) c.profile_t[k] = u53_threshold(cdf[k] / cdf[4]);
   }
   c.n_rules = in.n_rules;
   if (in.n_rules < 0 || in.n_rules > PGTG_MAX_RULES) return fail(h, PGTG_E_INVALID, "bad rule count");
@@ -1877,6 +1939,9 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     memcpy(t.lane_route, hs::kLaneRoute, sizeof t.lane_route);
     memcpy(t.route_type_lane, hs::kRouteTypeLane, sizeof t.route_type_lane);
     for (int r = 0; r < cfg->n_rules && r < PGTG_MAX_RULES; r++) memcpy(t.rule_w[r], cfg->rules[r].weight, sizeof t.rule_w[r]);
+    memcpy(t.beh_t, h->hcfg.beh_t, sizeof t.beh_t);
+    memcpy(t.beh_mf, h->hcfg.beh_min_follow, sizeof t.beh_mf);
+    memcpy(t.beh_pt, h->hcfg.beh_patience_thr, sizeof t.beh_pt);
     if ((rc = dalloc(h, &h->dtab, 1)) || hipMemcpy(h->dtab, &t, sizeof t, hipMemcpyHostToDevice) != hipSuccess) {
       g_create_err = "table upload failed";
       pgtg_destroy(h);
@@ -1998,6 +2063,11 @@ int pgtg_random_actions(pgtg_handle* h, uint8_t* actions_dev, uint64_t seed, uin
   return PGTG_OK;
 }
 
+static int read_traf(pgtg_handle* h, uint64_t env, uint4* t) {
+  HIPCHK(h, hipMemcpy(t, h->S.traf + env, sizeof *t, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int pgtg_get_env_state(pgtg_handle* h, uint64_t env, PgtgEnvState* st) {
   if (!h || !st || env >= h->n) return PGTG_E_INVALID;
   HIPCHK(h, hipSetDevice(h->device));
@@ -2023,13 +2093,15 @@ int pgtg_get_env_state(pgtg_handle* h, uint64_t env, PgtgEnvState* st) {
   st->used_subgoals = (uint64_t)r.b.z | ((uint64_t)r.b.w << 32);
   st->seed = seed;
   st->error = -(int)e;
+  if (h->hcfg.need_car) {
+    uint4 t;
+    if (int rc = read_traf(h, env, &t)) return rc;
+    st->n_cars = (int)(t.x & 0xffffu);
+    st->next_car_id = (int)t.y;
+  }
   return PGTG_OK;
 }
 
-static int read_traf(pgtg_handle* h, uint64_t env, uint4* t) {
-  HIPCHK(h, hipMemcpy(t, h->S.traf + env, sizeof *t, hipMemcpyDeviceToHost));
-  return 0;
-}
 
 int pgtg_get_cars(pgtg_handle* h, uint64_t env, PgtgCar* cars, int32_t cap, int32_t* n) {
   if (!h || env >= h->n || !n) return PGTG_E_INVALID;
@@ -2157,6 +2229,12 @@ int pgtg_read_stamps(uint64_t* out, uint64_t n) {
 
 int pgtg_window(const pgtg_handle* h) { return h ? h->hcfg.win : 0; }
 uint64_t pgtg_num_envs(const pgtg_handle* h) { return h ? h->n : 0; }
+int pgtg_launch_info(const pgtg_handle* h, int32_t* envs_per_block, int32_t* lds_bytes) {
+  if (!h) return PGTG_E_INVALID;
+  if (envs_per_block) *envs_per_block = h->L.envs;
+  if (lds_bytes) *lds_bytes = (int32_t)(h->lds + sizeof(Tables));
+  return PGTG_OK;
+}
 const char* pgtg_last_error(const pgtg_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
 
 int pgtg_enable_timing(pgtg_handle* h, int32_t on) {

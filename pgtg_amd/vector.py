@@ -220,6 +220,17 @@ class PGTGVecEnv:
     def add_car(self, i: int, x: int, y: int, route: int, profile: int):
         _check(self._lib.pgtg_add_car(self._h, i, x, y, route, profile), self._h)
 
+    def mean_cars(self, sample: int = 64) -> float:
+        """Average car count over (up to) `sample` envs (host-synchronising)."""
+        idx = range(0, self.num_envs, max(1, self.num_envs // sample))
+        return sum(self.env_state(i)["n_cars"] for i in idx) / len(idx)
+
+    def launch_info(self) -> tuple[int, int]:
+        """(envs per workgroup, LDS bytes per workgroup) of the step kernel."""
+        e, b = C.c_int32(), C.c_int32()
+        _check(self._lib.pgtg_launch_info(self._h, C.byref(e), C.byref(b)), self._h)
+        return e.value, b.value
+
     def counters(self) -> tuple[int, int]:
         a, b = C.c_uint64(), C.c_uint64()
         _check(self._lib.pgtg_get_counters(self._h, C.byref(a), C.byref(b)), self._h)

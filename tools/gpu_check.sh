@@ -5,7 +5,7 @@ TAG=${1:-dev}
 mkdir -p gpurun_out
 timeout -k 10 600 python -m pytest tests -m gpu -x -q 2>&1 | tail -15
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"
-for W in cfg2 cfg4 cfg5; do
+for W in cfg2 cfg4 cfg5 cfg3; do
   timeout -k 10 300 python bench.py --workload $W --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/bench_${TAG}_$W.json
   python -c "import json; d=json.load(open('gpurun_out/bench_${TAG}_$W.json')); r=d['roofline']; print('$W', f\"{d['value']/1e6:.1f}M env-steps/s\", f\"kernel {r['avg_kernel_us']:.1f}us\", f\"{r['achieved']:.1f} GB/s frac {r['frac']:.4f}\")"
 done

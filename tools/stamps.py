@@ -1,4 +1,9 @@
-"""Diagnostic: per-phase wave cycles of k_env from the -DPGTG_STAMPS build (not the product)."""
+"""Diagnostic: per-phase wave cycles of k_env from the -DPGTG_STAMPS build (not the product).
+
+Build: hipcc <pgtg_amd.build.FLAGS> -DPGTG_STAMPS -o pgtg_amd/libpgtg_hip_stamps.so pgtg_amd/csrc/pgtg_env.hip
+Usage: python tools/stamps.py [cfg2|cfg5|cfg3 ...]
+Only waves holding env lanes are summarised; a sub-phase is averaged over the waves whose lane 0
+executed it in the last launch (its stamps lie inside that wave's launch window)."""
 import ctypes as C
 import os
 import sys
@@ -12,25 +17,39 @@ from pgtg_amd import _abi  # noqa: E402
 _abi.LIB_PATH = os.path.join(os.path.dirname(_abi.LIB_PATH), "libpgtg_hip_stamps.so")
 from pgtg_amd.vector import PGTGVecEnv  # noqa: E402
 
-names = ["stage", "step", "final", "reset", "store", "obs"]
-for N, kw in [(4096, dict(random_map_width=3, random_map_height=3)),
-              (131072, dict(random_map_width=5, random_map_height=5))]:
+SLOTS = 32
+PHASES = ["stage", "step", "final", "reset", "store", "obs"]
+SUB = {"cars": (16, 17), "braking": (17, 18), "reset.seed": (8, 9), "reset.generate": (9, 10),
+       "reset.compile": (10, 11), "reset.start": (11, 12), "gen.start_goal": (9, 13), "gen.edge_init": (13, 14),
+       "gen.removal": (14, 15), "gen.tiles": (15, 10), "traf.spawners": (19, 20), "traf.floyd": (20, 21),
+       "traf.shuffle": (21, 22), "traf.create": (22, 23)}
+CASES = {"cfg2": (4096, dict(random_map_width=3, random_map_height=3)),
+         "cfg5": (131072, dict(random_map_width=5, random_map_height=5)),
+         "cfg3": (65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5))}
+for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
+    N, kw = CASES[name]
     env = PGTGVecEnv(N, device=0, **kw)
+    E, lds = env.launch_info()
     env.reset(seed=0)
     for k in range(30):
         env.step_random(1, k)
     torch.cuda.synchronize()
-    E = 64 if N <= 65536 else 256
-    nw = (N + E - 1) // E * 4
-    buf = np.zeros(nw * 16, np.uint64)
+    blocks = (N + E - 1) // E
+    nw = blocks * 4
+    buf = np.zeros(nw * SLOTS, np.uint64)
     _abi.lib().pgtg_read_stamps.argtypes = [C.c_void_p, C.c_uint64]
     _abi.lib().pgtg_read_stamps(buf.ctypes.data, buf.size)
-    st = buf.reshape(nw, 16).astype(np.int64)
+    st = buf.reshape(nw, SLOTS).astype(np.int64)
+    active = (np.arange(nw) % 4) * 64 < E
+    st = st[active]
     d = np.diff(st[:, :7], axis=1)
-    print(N, kw, "mean cycles per phase:", {n: int(x) for n, x in zip(names, d.mean(0))},
-          "total", int((st[:, 6] - st[:, 0]).mean()), flush=True)
-    f = np.diff(st[:, 8:13], axis=1)
-    print("   reset (waves with a reset):", {n: int(x) for n, x in zip(["seed", "generate", "compile", "start"], f.mean(0))}, flush=True)
-    g = st[:, [9, 13, 14, 15, 10]]
-    print("   generate:", {n: int(x) for n, x in zip(["start/goal", "edge init", "removal loop", "tiles+border+obst"], np.diff(g, axis=1).mean(0))}, flush=True)
+    print(f"{name}: {N} envs, {E} envs/workgroup, LDS {lds} B; cycles per active wave (last launch)", flush=True)
+    print("  phases:", {n: int(x) for n, x in zip(PHASES, d.mean(0))}, "total", int((st[:, 6] - st[:, 0]).mean()))
+    lo, hi = st[:, 0], st[:, 6]
+    out = {}
+    for n, (a, b) in SUB.items():
+        ok = (st[:, a] >= lo) & (st[:, a] <= hi) & (st[:, b] >= st[:, a]) & (st[:, b] <= hi)
+        if ok.any():
+            out[n] = (int((st[ok, b] - st[ok, a]).mean()), round(float(ok.mean()), 2))
+    print("  sub-phases (mean cycles, fraction of waves):", out, flush=True)
     env.close()
