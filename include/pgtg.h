@@ -134,6 +134,7 @@ typedef struct {
   int32_t n_cars, next_car_id, path_len, error;
   uint32_t spawn_counter;
   uint64_t seed, used_subgoals;
+  int32_t n_spawners, reserved;
 } PgtgEnvState;
 
 typedef struct {

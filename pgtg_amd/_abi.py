@@ -74,7 +74,8 @@ class PgtgOutputs(C.Structure):
 class PgtgEnvState(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("x", "y", "vx", "vy", "terminated", "flat_tire", "phase", "elapsed",
                                          "n_cars", "next_car_id", "path_len", "error")] + [
-        ("spawn_counter", C.c_uint32), ("seed", C.c_uint64), ("used_subgoals", C.c_uint64)]
+        ("spawn_counter", C.c_uint32), ("seed", C.c_uint64), ("used_subgoals", C.c_uint64),
+        ("n_spawners", C.c_int32), ("reserved", C.c_int32)]
 
 
 class PgtgCar(C.Structure):

@@ -16,6 +16,7 @@ constexpr int kMaxBorder = 192;   // border-connection candidates (<= 2w+2h-2)
 constexpr int kMaxWin = PGTG_MAX_WINDOW;
 constexpr int kMaskWords = (kMaxWin * kMaxWin + 31) / 32;  // 8
 constexpr int kBlock = 256;       // lanes (= envs) per workgroup for the step kernels
+constexpr int kSpCache = 32;      // spawner-list entries k_env keeps in LDS (the rest are read from HBM)
 
 // agent flags (EnvRec.w2 bits 16..23)
 constexpr uint32_t kFlagTerminated = 1u << 0;
@@ -72,10 +73,13 @@ struct DevCfg {
   // random() < p  <=>  (next64 >> 11) < ceil(p * 2^53): probabilities as integer thresholds
   uint64_t beh_t[5][5];  // [BEH_*][profile]
   int32_t beh_min_follow[5], beh_patience_thr[5];  // patience > level*10  <=>  patience > floor(level*10)
-  int32_t traf_bytes;      // per-lane LDS traffic region (occupancy counters / reset scratch)
-  int32_t floyd_out_off;   // byte offsets inside it used during traffic_reset
-  int32_t floyd_seen_off;
-  int32_t floyd_pre_off;
+  int32_t traf_bytes;      // k_env per-lane LDS traffic region: occupancy counters, spawner cache
+  int32_t sp_cache_off;    // byte offset of the spawner cache (kSpCache entries) in it
+  int32_t rs_bytes;        // k_traffic per-lane reset scratch: Floyd output [0, 2*cap), seen set, column prefix
+  int32_t rs_seen_off;
+  int32_t rs_pre_off;
+  int32_t traffic_ch;      // index of the traffic channel in the observation, -1 if absent
+  int32_t obs_fast;        // observation window == the agent's tile (k_traffic patches its traffic bits)
   int32_t manual_cars;     // cars may be added through pgtg_add_car
   int32_t n_rules;
   PgtgRule rules[PGTG_MAX_RULES];
@@ -106,7 +110,7 @@ struct Tables {
   uint16_t spcol[16][9];
   uint16_t allcol[16][4][9];
   uint8_t lane_route[32];
-  uint8_t route_type_lane[20][4];
+  alignas(4) uint8_t route_type_lane[20][4];  // read as one word per route
   uint8_t rule_w[PGTG_MAX_RULES][6][20];
   // DRIVER_BEHAVIORS per profile, read per car by profile index (kept in LDS, not in the DevCfg
   // constant block, so a per-lane index never becomes a dependent global load)
@@ -140,6 +144,8 @@ struct DevState {
   uint32_t* car_id;
   uint4* traf;
   uint16_t* spawners;     // [max_spawners][n] square codes x | y<<8, x-major order
+  uint32_t* tr_list;      // [n] envs k_env reset this launch (k_traffic's work list)
+  uint32_t* tr_count;     // [2] list lengths, alternating launches
   uint8_t* err;           // [n] last error code (negated PGTG_E_*)
   unsigned long long* counters;  // [2]: env steps, episodes
   const int8_t* nsd_tab;
@@ -157,6 +163,11 @@ struct Pcg {
 };
 
 __device__ __forceinline__ void pcg_step(Pcg& g) {
+#ifdef PGTG_ABL_CHEAP_RNG  // diagnostic timing build only: NOT numpy's stream
+  g.slo = g.slo * 0x9E3779B97F4A7C15ull + g.ilo;
+  g.shi ^= g.slo;
+  return;
+#endif
   const uint64_t MH = 0x2360ED051FC65DA4ull, ML = 0x4385DF649FCCF645ull;
   uint64_t lo = g.slo * ML;
   uint64_t hi = __umul64hi(g.slo, ML) + g.slo * MH + g.shi * ML;
@@ -201,6 +212,36 @@ __device__ __forceinline__ uint32_t pcg_int(Pcg& g, uint32_t n) {
   }
   return (uint32_t)(m >> 32);
 }
+// One draw of a per-lane sequence whose kind differs between lanes: random()'s 53-bit mantissa or
+// integers(0, n) (Lemire on next_uint32 with the high-half buffer).  Callers skip the draw for
+// integer draws with n <= 1 (numpy draws nothing there).  Keeping one PCG step site per draw slot
+// instead of one per distribution keeps a divergent wave's instruction stream short.
+__device__ __forceinline__ uint64_t pcg_draw(Pcg& g, bool is_int, uint32_t n) {
+  const bool step = !is_int || !g.has;
+  uint64_t v = 0;
+  if (step) v = pcg_next64(g);
+  if (!is_int) return v >> 11;
+  uint32_t r32;
+  if (step) {
+    r32 = (uint32_t)v;
+    g.has = 1;
+    g.buf = (uint32_t)(v >> 32);
+  } else {
+    r32 = g.buf;
+    g.has = 0;
+  }
+  uint64_t m = (uint64_t)r32 * n;
+  uint32_t left = (uint32_t)m;
+  if (left < n) {
+    const uint32_t thr = (0xffffffffu - (n - 1u)) % n;
+    while (left < thr) {
+      m = (uint64_t)pcg_next32(g) * n;
+      left = (uint32_t)m;
+    }
+  }
+  return m >> 32;
+}
+
 // choice(k, p=p) with the host-normalised CDF (cumsum(p)/cumsum[-1]) as 53-bit thresholds:
 // searchsorted(u, 'right') counts the entries <= u
 template <int K>

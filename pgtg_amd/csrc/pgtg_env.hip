@@ -485,11 +485,11 @@ __device__ __forceinline__ uint32_t spawner_colmask(const DevCfg& c, uint32_t ex
 }
 
 // Initial traffic of a fresh episode (EpisodeMap scans pgtg/map.py:31-42 and
-// _create_initial_traffic pgtg/environment.py:830-879).  `tr` is the lane's LDS traffic region:
-// layout: occupancy counters [0, nt*32), then Floyd's output, its seen set and the column prefix,
-// so the counters are built while the cars are created.
+// _create_initial_traffic pgtg/environment.py:830-879), run by k_traffic for the envs k_env reset.
+// `rs` is the lane's LDS reset scratch: Floyd's output [0, 2*cap), its seen set and the per-column
+// prefix of spawnable squares.  CR collects the new cars on the agent's tile `at` (observation).
 __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S, uint64_t i, const Plan& pl,
-                                             Pcg& cr, uint8_t* tr, TrafState& ts) {
+                                             Pcg& cr, uint8_t* rs, TrafState& ts, int at, uint32_t* CR) {
   const uint64_t N = S.n;
   STAMP(19);
   // car spawners in x-major order -> HBM list
@@ -507,7 +507,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
     }
   }
   // spawnable positions (squares holding any car lane), x-major: per-column prefix counts
-  uint16_t* colpre = reinterpret_cast<uint16_t*>(tr + c.floyd_pre_off);
+  uint16_t* colpre = reinterpret_cast<uint16_t*>(rs + c.rs_pre_off);
   int np = 0;
   for (int x = 0; x < c.W; x++) {
     int tx = x / kTile, lx = x - tx * kTile;
@@ -521,12 +521,11 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
   const int ncars = (int)((double)np * c.density);  // int(len(positions) * traffic_density)
   int k = 0;
   CarStore cs{S.car_w0, S.car_w1, S.car_id, N, i};
-  for (int w = 0; w < c.nt * 8; w++) reinterpret_cast<uint32_t*>(tr)[w] = 0u;
   if (ncars > 0 && np > 0) {
     k = min(ncars, np);
     if (k > c.car_cap) return PGTG_E_UNSUPPORTED;
-    uint16_t* out = reinterpret_cast<uint16_t*>(tr + c.floyd_out_off);
-    uint32_t* seen = reinterpret_cast<uint32_t*>(tr + c.floyd_seen_off);
+    uint16_t* out = reinterpret_cast<uint16_t*>(rs);
+    uint32_t* seen = reinterpret_cast<uint32_t*>(rs + c.rs_seen_off);
     for (int w = 0; w < (np + 31) / 32; w++) seen[w] = 0u;
     STAMP(20);
     // Generator.choice(np, k, replace=False): Floyd's algorithm, then _shuffle_int
@@ -552,16 +551,22 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
         int mid = (lo + hi) >> 1;
         if (colpre[mid] <= idx) lo = mid; else hi = mid;
       }
-      int x = lo, rr = idx - colpre[x], tx = x / kTile, lx = x - tx * kTile, y = 0;
+      int x = lo, rr = idx - colpre[x], tx = x / kTile, lx = x - tx * kTile, y = 0, t_car = -1, ly = 0;
       for (int ty = 0; ty < c.th; ty++) {
         uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
         uint32_t msk = ex ? sT.lanecol[ex][lx] : 0u;
         int cnt = __popc(msk);
         if (rr < cnt) {
-          y = ty * kTile + kth_bit(msk, rr);
+          ly = kth_bit(msk, rr);
+          y = ty * kTile + ly;
+          t_car = ty * c.tw + tx;
           break;
         }
         rr -= cnt;
+      }
+      if (t_car == at) {
+        const int sq = lx * 9 + ly;
+        CR[sq >> 5] |= 1u << (sq & 31);
       }
       uint32_t rl = square_lanes(c, pl, x, y) & 0x0fffffffu;
       int nr = __popc(rl);
@@ -572,8 +577,6 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
       cs.w0[a] = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
       cs.w1[a] = 0u;
       cs.id[a] = (uint32_t)m;
-      const int sl = lane_slot(c, pl, x, y);
-      if (sl < 0 || !occ_inc(tr, sl)) return PGTG_E_UNSUPPORTED;
     }
   }
   STAMP(23);
@@ -587,7 +590,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
 // The full per-env reset.  `key` = spawn counter (5 children per episode).  Returns 0 or -code.
 template <bool TR>
 __device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, uint16_t* plan,
-                                         uint8_t* q, uint8_t* par, uint8_t* tr, TrafState& ts) {
+                                         uint8_t* q, uint8_t* par, TrafState& ts) {
   STAMP(8);
   uint64_t seed = S.seed[i];
   SeedPool sp = ss_pool(seed);
@@ -642,11 +645,9 @@ __device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uin
     int b = (v.px + 2) * c.vis_pitch + (v.py + 2);
     vis[b >> 5] |= 1u << (b & 31);
   }
-  if ((TR && c.need_car)) {
-    Plan pl{plan};
-    int e = traffic_reset(c, S, i, pl, car_rng, tr, ts);
+  if ((TR && c.need_car)) {  // the cars are created by k_traffic from this stream
     stream_store_all(S.car, i, car_rng);
-    if (e) return e;
+    ts = TrafState{0, 0, 0, 0};
   }
   return 0;
 }
@@ -747,7 +748,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
     int gl_t = (int)((v.sg >> 16) & 0xffu), gl_d = (int)(v.sg >> 24);
     uint32_t ot = plan_otype(p);
     uint32_t CR[3] = {0, 0, 0};  // squares of this tile holding a car
-    if ((TR && c.need_car) && ex) {
+    if ((TR && c.need_car) && occ && ex) {
       for (int sl = 0; sl < 32; sl++) {
         if (occ[t * 32 + sl]) {
           int sq = sT.slot_sq[ex][sl];
@@ -798,7 +799,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
       for (int w0 = 0; w0 < WW; w0 += 32) {
         uint32_t acc = 0;
         if (code == PGTG_CH_TRAFFIC) {
-          if ((TR && c.need_car)) {
+          if ((TR && c.need_car) && occ) {
             int nb = min(32, WW - w0);
             for (int b = 0; b < nb; b++) {
               int bb = w0 + b, ii = bb / win, j = bb - ii * win;
@@ -859,12 +860,23 @@ struct BrakeQuery {
 // _get_next_car_position_and_route :881-968, _should_car_move :678-691, traffic lights :664-676,
 // _spawn_new_car :970-1002).  Survivors go to the other bank in order, respawned cars are appended
 // after them in creation order; occupancy counters follow every move so later cars see earlier ones.
+template <typename T>
+__device__ __forceinline__ T sel4(int k, T a0, T a1, T a2, T a3) {
+  return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
+}
+
+// The per-car work is organised for a divergent wave: every map lookup the car may need (its slot,
+// the four neighbours, the first admissible one, light and occupancy there) is computed branch-free
+// first; the random draws then go through five draw slots shared by all outcomes (a lane's draws
+// keep numpy's order: delay?, delay length | speed, route | spawner | light, go | profile, route).
 __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uint64_t i, const EnvView& v,
                                          const Plan& pl, uint8_t* occ, const uint16_t* sp, TrafState& ts, Pcg& cr,
                                          int color, BrakeQuery& bq, uint8_t* hist) {
   CarStore cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
   const int cap = c.car_cap, cur = (int)ts.bank, nxt = cur ^ 1;
   const int n0 = (int)ts.n_cars;
+  const int tw = c.tw, th = c.th;
+  const uint32_t nsp = ts.n_spawners;
   int w = 0, nnew = 0;
   // software pipeline: the next car's words are requested before the current car is processed, so
   // their HBM latency overlaps this car's work (the loop-carried copy waits only at the iteration end)
@@ -886,85 +898,83 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
     }
     const int x = (int)(a & 255u), y = (int)((a >> 8) & 255u), prof = (int)((a >> 21) & 7u);
     int route = (int)((a >> 16) & 31u), delay = (int)((a >> 24) & 3u);
-    int nx = x, ny = y;
-    bool remove = false;
-    bool move;
-    if (delay > 0) {
+    // ---- map lookups (no draws)
+    const int tx = x / kTile, ty = y / kTile, lx = x - tx * kTile, ly = y - ty * kTile;
+    const int t0 = ty * tw + tx, sq = lx * 9 + ly;
+    const int s_old = t0 * 32 + sT.li[plan_exits(pl[t0])][sq];
+    // neighbours up, down, left, right (_get_next_car_position_and_route's order)
+    const bool ok0 = !(ly == 0 && ty == 0), ok1 = !(ly == 8 && ty == th - 1);
+    const bool ok2 = !(lx == 0 && tx == 0), ok3 = !(lx == 8 && tx == tw - 1);
+    const int nt0 = ly == 0 ? t0 - tw : t0, nt1 = ly == 8 ? t0 + tw : t0;
+    const int nt2 = lx == 0 ? t0 - 1 : t0, nt3 = lx == 8 ? t0 + 1 : t0;
+    const int nq0 = ly == 0 ? sq + 8 : sq - 1, nq1 = ly == 8 ? sq - 8 : sq + 1;
+    const int nq2 = lx == 0 ? sq + 72 : sq - 9, nq3 = lx == 8 ? sq - 72 : sq + 9;
+    const uint32_t e0 = ok0 ? plan_exits(pl[nt0]) : 0u, e1 = ok1 ? plan_exits(pl[nt1]) : 0u;
+    const uint32_t e2 = ok2 ? plan_exits(pl[nt2]) : 0u, e3 = ok3 ? plan_exits(pl[nt3]) : 0u;
+    const uint32_t l0 = e0 ? sT.lanes[e0][nq0] : 0u, l1 = e1 ? sT.lanes[e1][nq1] : 0u;
+    const uint32_t l2 = e2 ? sT.lanes[e2][nq2] : 0u, l3 = e3 ? sT.lanes[e3][nq3] : 0u;
+    const uint32_t rtl = *reinterpret_cast<const uint32_t*>(sT.route_type_lane[route]);
+    int dec = -1;
+    bool dec_all = false;
+#pragma unroll
+    for (int t = 3; t >= 0; t--) {  // the first direction with a lane "all <t>" or the route's lane
+      const uint32_t ln = sel4(t, l0, l1, l2, l3);
+      const bool all = (ln >> (28 + t)) & 1u;
+      const uint32_t lane = (rtl >> (8 * t)) & 255u;
+      const bool rt = lane != 255u && ((ln >> lane) & 1u);
+      if (all || rt) {
+        dec = t;
+        dec_all = all;
+      }
+    }
+    const int dk = dec < 0 ? 0 : dec;
+    const int tg_t = sel4(dk, nt0, nt1, nt2, nt3), tg_q = sel4(dk, nq0, nq1, nq2, nq3);
+    const uint32_t tg_ln = sel4(dk, l0, l1, l2, l3);
+    const uint32_t p_tg = pl[dec < 0 ? t0 : tg_t];
+    const uint32_t ex_tg = plan_exits(p_tg);
+    const bool tl = plan_otype(p_tg) == 4u && !bit81(sT.wall[ex_tg], tg_q) && bit81(sT.obst[plan_omask(p_tg)], tg_q);
+    const int s_tg = tg_t * 32 + sT.li[ex_tg][tg_q];
+    const int occ_tg = dec < 0 ? 0 : occ[s_tg];
+    // ---- draws (_should_car_move, route choice / light / following, _spawn_new_car)
+    const bool act = delay == 0;
+    bool delayed = false, move = false;
+    if (act) {
+      delayed = pcg_draw(cr, false, 0u) < sT.beh_t[BEH_DELAY][prof];
+      const uint64_t r2 = pcg_draw(cr, delayed, 3u);
+      if (delayed) delay = 1 + (int)r2;  // integers(1, 4)
+      else move = r2 < sT.beh_t[BEH_SPEED][prof];
+    } else {
       delay -= 1;
-      move = false;
-    } else if (pcg_u53(cr) < sT.beh_t[BEH_DELAY][prof]) {
-      delay = 1 + (int)pcg_int(cr, 3);  // integers(1, 4)
-      move = false;
-    } else {
-      move = pcg_u53(cr) < sT.beh_t[BEH_SPEED][prof];
     }
-    if (!move) {
-      pat += 1;
-    } else {
-      bool decided = false;
-      for (int t = 0; t < 4 && !decided; t++) {  // up, down, left, right
-        const int px = x + (t == 2 ? -1 : t == 3 ? 1 : 0), py = y + (t == 0 ? -1 : t == 1 ? 1 : 0);
-        if (!inside(c, px, py)) continue;
-        const uint32_t ln = square_lanes(c, pl, px, py);
-        if ((ln >> (28 + t)) & 1u) {  // "car_lane all <type>": enter with a new random route
-          const uint32_t rl = ln & 0x0fffffffu;
-          const int nr = __popc(rl);
-          if (nr == 0) return PGTG_E_MAP;  // numpy choice([]) raises
-          route = sT.lane_route[kth_bit(rl, (int)pcg_int(cr, (uint32_t)nr))];
-          pat = 0;
-          nx = px;
-          ny = py;
-          decided = true;
-        } else {
-          const int lane = sT.route_type_lane[route][t];
-          if (lane != 255 && ((ln >> lane) & 1u)) {
-            decided = true;
-            bool stop = false;
-            if (square_tlight(c, pl, px, py)) {
-              if (color == 1) stop = pcg_u53(cr) < sT.beh_t[BEH_YELLOW][prof];
-              else if (color == 2) stop = !(pcg_u53(cr) < sT.beh_t[BEH_RED][prof]);
-            }
-            if (stop) {
-              pat += 1;
-            } else if (occ_at(c, pl, occ, px, py) > 0) {
-              bool go = false;
-              if (sT.beh_mf[prof] == 0 || (int)pat > sT.beh_pt[prof])
-                go = pcg_u53(cr) < sT.beh_t[BEH_GO][prof];
-              if (go) {
-                pat = 0;
-                nx = px;
-                ny = py;
-              } else {
-                pat += 1;
-              }
-            } else {
-              pat = 0;
-              nx = px;
-              ny = py;
-            }
-          }
-        }
-      }
-      if (!decided) {
-        pat += 1;
-        remove = true;
-      }
-    }
-    const int s_old = lane_slot(c, pl, x, y);
-    if (remove) {
-      occ[s_old]--;
+    const int kind = !move ? 0 : (dec < 0 ? 3 : (dec_all ? 1 : 2));  // stay, all-lane, route lane, respawn
+    const uint32_t nr_all = __popc(tg_ln & 0x0fffffffu);
+    if (kind == 1 && nr_all == 0) return PGTG_E_MAP;  // numpy choice([]) raises
+    const bool lit = kind == 2 && tl && color != 0;
+    const bool s3_int = kind != 2;
+    const uint32_t s3_n = kind == 1 ? nr_all : nsp;
+    uint64_t r3 = 0;
+    if ((kind == 1 || kind == 3 || lit) && !(s3_int && s3_n <= 1u)) r3 = pcg_draw(cr, s3_int, s3_n);
+    const bool stop = lit && (color == 1 ? r3 < sT.beh_t[BEH_YELLOW][prof] : !(r3 < sT.beh_t[BEH_RED][prof]));
+    const bool go_try = kind == 2 && !stop && occ_tg > 0 && (sT.beh_mf[prof] == 0 || (int)pat > sT.beh_pt[prof]);
+    uint64_t r4 = 0;
+    if (go_try || kind == 3) r4 = pcg_draw(cr, false, 0u);
+    if (kind == 3) {
       // _spawn_new_car: choice(car_spawners) -> sorted routes -> profile -> route
+      occ[s_old]--;
       int sx = 0, sy = 0;
-      if (ts.n_spawners > 0) {
-        uint32_t code = sp[pcg_int(cr, ts.n_spawners)];
+      if (nsp > 0) {
+        const uint32_t code = r3 < (uint64_t)kSpCache ? sp[r3] : S.spawners[r3 * S.n + i];
         sx = (int)(code & 255u);
         sy = (int)(code >> 8);
       }
       const uint32_t rl = square_lanes(c, pl, sx, sy) & 0x0fffffffu;
-      const int nr = __popc(rl);
-      const int nprof = pcg_choice_cdf<5>(cr, c.profile_t);
+      const uint32_t nr = __popc(rl);
+      int nprof = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) nprof += (r4 < c.profile_t[j]) ? 0 : 1;
       if (nr == 0) return PGTG_E_MAP;
-      const int nroute = sT.lane_route[kth_bit(rl, (int)pcg_int(cr, (uint32_t)nr))];
+      const uint32_t r5 = nr > 1u ? (uint32_t)pcg_draw(cr, true, nr) : 0u;
+      const int nroute = sT.lane_route[kth_bit(rl, (int)r5)];
       const uint64_t an = cs.at(nxt, cap, n0 - 1 - nnew);
       cs.w0[an] = (uint32_t)sx | (uint32_t)sy << 8 | (uint32_t)nroute << 16 | (uint32_t)nprof << 21;
       cs.w1[an] = 0u;
@@ -977,11 +987,19 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
         hist[nroute]++;
       }
     } else {
-      int s_cur = s_old;
-      if (nx != x || ny != y) {
+      const bool go = go_try && r4 < sT.beh_t[BEH_GO][prof];
+      const bool moved = kind == 1 || (kind == 2 && !stop && (occ_tg == 0 || go));
+      if (kind == 1) route = sT.lane_route[kth_bit(tg_ln & 0x0fffffffu, (int)r3)];
+      int nx = x, ny = y, s_cur = s_old;
+      if (moved) {
+        nx = x + (dk == 2 ? -1 : (dk == 3 ? 1 : 0));
+        ny = y + (dk == 0 ? -1 : (dk == 1 ? 1 : 0));
         occ[s_old]--;
-        s_cur = lane_slot(c, pl, nx, ny);
+        s_cur = s_tg;
         if (!occ_inc(occ, s_cur)) return PGTG_E_UNSUPPORTED;
+        pat = 0;
+      } else {
+        pat += 1;
       }
       if (bq.tile >= 0 && (s_cur >> 5) == bq.tile) {
         bq.n_in++;
@@ -1281,7 +1299,7 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   Lds l;
   l.envs = envs;
   l.plan_stride_dw = odd_up((c.nt + 1) / 2);
-  l.scratch_dw = odd_up((2 * c.nt + 3) / 4);
+  l.scratch_dw = c.need_car ? 0 : odd_up((2 * c.nt + 3) / 4);  // with traffic: inside the counters
   l.traf_dw = c.need_car ? odd_up(c.traf_bytes / 4) : 0;
   l.hist_dw = c.n_rules > 0 ? 5 : 0;
   l.seg_words = c.n_channels * c.mask_words;
@@ -1338,11 +1356,14 @@ __device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, con
 template <bool TR>
 __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
                                                  DevState S, const uint8_t* __restrict__ actions,
-                                                 const uint8_t* __restrict__ mask, PgtgOutputs out, int mode, Lds L) {
+                                                 const uint8_t* __restrict__ mask, PgtgOutputs out, int mode, Lds L,
+                                                 uint32_t tr_slot) {
   extern __shared__ uint32_t lds[];
   const DevCfg& c = *cfg;
   const int tid = threadIdx.x;
   STAMP(0);
+  // the traffic-reset list of the next launch starts empty (its previous consumer has finished)
+  if ((TR && c.need_car) && mode != MODE_OBSERVE && blockIdx.x == 0 && tid == 0) S.tr_count[tr_slot ^ 1u] = 0u;
   // stage the lane-indexed tables (kLanes only when a pass needs it)
   {
     const int words = (int)((c.generic_channels || (TR && c.need_car) ? sizeof(Tables) : offsetof(Tables, lanes)) / 4);
@@ -1362,10 +1383,11 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   uint32_t* st = lds + L.envs * (L.plan_stride_dw + L.scratch_dw + L.traf_dw + L.hist_dw);
   uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
   uint8_t* occ = reinterpret_cast<uint8_t*>(traf_w);
-  uint16_t* sp_l = reinterpret_cast<uint16_t*>(occ + c.floyd_out_off);  // spawner list during the step
+  uint16_t* sp_l = reinterpret_cast<uint16_t*>(occ + c.sp_cache_off);  // first spawners of the list
   uint8_t* hist = reinterpret_cast<uint8_t*>(hist_w);
   Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
-  uint8_t* q = reinterpret_cast<uint8_t*>(scr_w);
+  // the map reset's BFS scratch reuses the occupancy counters, which are dead by then
+  uint8_t* q = (TR && c.need_car) ? occ : reinterpret_cast<uint8_t*>(scr_w);
   uint8_t* par = q + c.nt;
 
   EnvView v{};
@@ -1407,8 +1429,8 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
         }
       }
     }
-    // the spawner list (respawn positions) into the reset-scratch part of the traffic region
-    const int nsp = (int)ts.n_spawners;
+    // the head of the spawner list (respawn positions) into LDS
+    const int nsp = min((int)ts.n_spawners, kSpCache);
     for (int k0 = 0; k0 < nsp; k0 += 8) {
       uint16_t s8[8];
 #pragma unroll
@@ -1457,11 +1479,13 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   }
   STAMP(3);
   const bool reset_now = my_sel != 0;
+  bool tr_push = false;
   const int n_resets = __syncthreads_count(reset_now);
   if (tid == 0 && n_resets) atomicAdd(&S.counters[1], (unsigned long long)n_resets);
   if (reset_now) {
-    int e2 = env_reset<TR>(c, S, i, v, pl.p, q, par, occ, ts);
+    int e2 = env_reset<TR>(c, S, i, v, pl.p, q, par, ts);
     if (e2) err = e2;
+    tr_push = (TR && c.need_car) && e2 == 0;
     uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
     for (int k = 0; k < c.plan_stride / 8; k++) {
       uint32_t wv[4];
@@ -1476,13 +1500,24 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       rec_store(S.rec, i, v);
       if ((TR && c.need_car)) S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.bank, 0u);
     }
-    S.err[i] = (uint8_t)(-err);
+    if (mode != MODE_OBSERVE || err) S.err[i] = (uint8_t)(-err);
+  }
+  if (TR && c.need_car) {
+    // k_traffic's work list: one wave-aggregated atomic per wave
+    const uint64_t m = __ballot(tr_push);
+    if (m) {
+      const int lane = tid & 63, leader = __ffsll((long long)m) - 1;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(&S.tr_count[tr_slot], (uint32_t)__popcll(m));
+      base = __shfl(base, leader);
+      if (tr_push) S.tr_list[base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
+    }
   }
   STAMP(5);
   if (single) {
     if (reset_now) {
       ObsInfo oi;
-      build_obs<TR>(c, S, pl, v, st + tid * L.seg_words, oi, occ);
+      build_obs<TR>(c, S, pl, v, st + tid * L.seg_words, oi, nullptr);  // cars come from k_traffic
       write_small_outputs(c, out, i, v, oi, false);
     }
     __syncthreads();
@@ -1490,10 +1525,66 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
                 (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, nullptr);
   } else {
-    obs_pass<TR>(c, S, pl, v, out, out.obs, env0, nb, live, false, nullptr, st, L, occ);
+    obs_pass<TR>(c, S, pl, v, out, out.obs, env0, nb, live, false, nullptr, st, L, reset_now ? nullptr : occ);
   }
   if (mode == MODE_STEP && tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
   STAMP(6);
+}
+
+// Initial traffic of the envs k_env reset in this launch (its work list), one lane per env with
+// the reset scratch in LDS; the observation k_env wrote for them gets the new cars' squares.
+__global__ void __launch_bounds__(64) k_traffic(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
+                                                DevState S, PgtgOutputs out, uint32_t tr_slot, int plan_dw, int rs_dw) {
+  extern __shared__ uint32_t lds[];
+  const DevCfg& c = *cfg;
+  const uint32_t n = S.tr_count[tr_slot];
+  const uint32_t j0 = blockIdx.x * blockDim.x;
+  if (j0 >= n) return;  // whole workgroup idle
+  const int tid = threadIdx.x;
+  {
+    const int words = (int)(sizeof(Tables) / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
+    uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
+    for (int k = tid; k < words; k += blockDim.x) dstt[k] = src[k];
+  }
+  __syncthreads();
+  const uint32_t j = j0 + tid;
+  if (j >= n) return;
+  const uint64_t i = S.tr_list[j];
+  uint32_t* plan_w = lds + tid * plan_dw;
+  uint8_t* rs = reinterpret_cast<uint8_t*>(lds + blockDim.x * plan_dw + tid * rs_dw);
+  const uint4* src = reinterpret_cast<const uint4*>(S.plan + i * (uint64_t)c.plan_stride);
+  for (int k = 0; k < c.plan_stride / 8; k++) {
+    uint4 w4 = src[k];
+    uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (k * 4 + q < plan_dw) plan_w[k * 4 + q] = wv[q];
+  }
+  Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
+  const EnvView v = rec_load(S.rec, i);
+  const int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
+  const int at = (piy / kTile) * c.tw + pix / kTile;
+  Pcg cr = stream_load(S.car, i);
+  TrafState ts{0, 0, 0, 0};
+  uint32_t CR[3] = {0u, 0u, 0u};
+  const int e = traffic_reset(c, S, i, pl, cr, rs, ts, at, CR);
+  stream_store_state(S.car, i, cr);
+  S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.bank, 0u);
+  if (e) S.err[i] = (uint8_t)(-e);
+  if (c.obs_fast && c.traffic_ch >= 0 && out.obs) {
+    // the tile window's traffic channel: k_env wrote it with no cars; set the car squares
+    uint8_t* o = out.obs + i * (uint64_t)c.obs_bytes + (uint64_t)c.traffic_ch * 81u;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      uint32_t m = CR[k];
+      while (m) {
+        const int b = __ffs((int)m) - 1;
+        m &= m - 1u;
+        o[k * 32 + b] = 1;
+      }
+    }
+  }
 }
 
 __global__ void k_random_actions(uint8_t* a, uint64_t n, uint64_t seed, uint64_t t) {
@@ -1539,6 +1630,11 @@ struct pgtg_handle {
   size_t ev_used = 0;
   double acc_ms = 0.0;
   uint64_t acc_n = 0;
+  // k_traffic: work-list parity, lanes per workgroup and dynamic LDS
+  uint32_t tr_slot = 0;
+  int kt_lanes = 64;
+  int kt_plan_dw = 0, kt_rs_dw = 0;
+  size_t kt_lds = 0;
 };
 
 
@@ -1751,6 +1847,10 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
   }
   c.mask_words = (c.win * c.win + 31) / 32;
   c.obs_bytes = c.n_channels * c.win * c.win;
+  c.traffic_ch = -1;
+  for (int k = 0; k < c.n_channels; k++)
+    if (c.channels[k] == PGTG_CH_TRAFFIC) c.traffic_ch = k;
+  c.obs_fast = !c.sliding && !c.generic_channels;
   // streams that can ever be drawn from (unobservable streams are never materialised)
   bool obst_possible = in.fixed_map ? false : in.obstacle_probability > 0;
   bool kinds[4] = {false, false, false, false};
@@ -1774,14 +1874,13 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
     if (cap < 1) cap = 1;
     c.car_cap = cap;
     c.max_spawners = c.nt * 5;
-    int out_off = c.nt * 32;  // occupancy counters first
-    const int out_n = cap > c.max_spawners ? cap : c.max_spawners;  // Floyd output / spawner list
-    int seen_off = out_off + ((2 * out_n + 3) / 4) * 4;
-    int pre_off = seen_off + 4 * c.nt;
-    c.floyd_out_off = out_off;
-    c.floyd_seen_off = seen_off;
-    c.floyd_pre_off = pre_off;
-    c.traf_bytes = (pre_off + 2 * (c.W + 1) + 3) / 4 * 4;
+    // k_env: occupancy counters (nt * 32 lane slots, u8) then the spawner cache
+    c.sp_cache_off = c.nt * 32;
+    c.traf_bytes = c.sp_cache_off + 2 * kSpCache;
+    // k_traffic: Floyd output (u16 x cap), seen bits of the spawnable squares (<= nt * 32), column prefix
+    c.rs_seen_off = ((2 * cap + 3) / 4) * 4;
+    c.rs_pre_off = c.rs_seen_off + 4 * c.nt;
+    c.rs_bytes = (c.rs_pre_off + 2 * (c.W + 1) + 3) / 4 * 4;
   }
   {  // DRIVER_BEHAVIORS (pgtg/environment.py:64-109)
     const double ys[5] = {0.95, 0.75, 0.3, 0.98, 0.1}, rv[5] = {0.01, 0.05, 0.15, 0.001, 0.3};
@@ -1880,6 +1979,8 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     ALLOC(S.car_id, 2 * (uint64_t)c.car_cap * n);
     ALLOC(S.traf, n);
     ALLOC(S.spawners, (uint64_t)c.max_spawners * n);
+    ALLOC(S.tr_list, n);
+    ALLOC(S.tr_count, 2);
   }
   // atan2 tables
   {
@@ -1956,11 +2057,33 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
   {
     // envs per 256-lane workgroup: small batches spread over more CUs with 4 lanes per env for
     // the observation writes; large batches keep a full workgroup of env lanes for occupancy.
-    int envs = n_envs <= (uint64_t)64 * 1024 ? 64 : kBlock;
+    // Traffic keeps 64 envs (one wave of car loops) per workgroup and sizes the observation
+    // sub-batch so that two workgroups share a CU's 160 KiB of LDS when the counters allow it.
+    int envs = (n_envs <= (uint64_t)64 * 1024 || c.need_car) ? 64 : kBlock;
     if (const char* e = getenv("PGTG_ENVS_PER_BLOCK")) envs = atoi(e);
-    if (envs != 64 && envs != 128 && envs != kBlock) envs = kBlock;
-    while (envs > 64 && lds_bytes(lds_layout(c, envs)) + sizeof(Tables) > 150 * 1024) envs /= 2;
+    if (envs != 16 && envs != 32 && envs != 64 && envs != 128 && envs != kBlock) envs = kBlock;
+    while (envs > 16 && lds_bytes(lds_layout(c, envs)) + sizeof(Tables) > 150 * 1024) envs /= 2;
     h->L = lds_layout(c, envs);
+    if (c.need_car) {
+      while (h->L.sub_envs > 8 && lds_bytes(h->L) + sizeof(Tables) > 80 * 1024) {
+        h->L.sub_envs /= 2;
+        h->L.stream_words = h->L.sub_envs * h->L.seg_words + 2;
+      }
+      // k_traffic: per-lane plan + reset scratch
+      h->kt_plan_dw = odd_up((c.nt + 1) / 2);
+      h->kt_rs_dw = odd_up(c.rs_bytes / 4);
+      h->kt_lanes = 64;
+      while (h->kt_lanes > 8 && (size_t)4 * h->kt_lanes * (h->kt_plan_dw + h->kt_rs_dw) + sizeof(Tables) > 150 * 1024)
+        h->kt_lanes /= 2;
+      h->kt_lds = (size_t)4 * h->kt_lanes * (h->kt_plan_dw + h->kt_rs_dw);
+      if (h->kt_lds + sizeof(Tables) > 160 * 1024) {
+        g_create_err = "LDS budget exceeded (traffic reset scratch)";
+        pgtg_destroy(h);
+        return PGTG_E_UNSUPPORTED;
+      }
+      if (h->kt_lds > 64 * 1024)
+        (void)hipFuncSetAttribute((const void*)k_traffic, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->kt_lds);
+    }
   }
   h->lds = lds_bytes(h->L);
   if (h->lds + sizeof(Tables) > 160 * 1024) {
@@ -2014,11 +2137,27 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
   }
   if (h->hcfg.need_car || h->hcfg.n_rules > 0)
     hipLaunchKernelGGL(k_env<true>, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
-                       actions, mask, h->out, mode, h->L);
+                       actions, mask, h->out, mode, h->L, h->tr_slot);
   else
     hipLaunchKernelGGL(k_env<false>, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
-                       actions, mask, h->out, mode, h->L);
+                       actions, mask, h->out, mode, h->L, h->tr_slot);
   HIPCHK(h, hipGetLastError());
+  if (h->hcfg.need_car && mode != MODE_OBSERVE) {
+    // initial traffic of the envs reset by this launch, then (windows other than the agent's tile)
+    // their observation again with the cars
+    const uint64_t kb = (h->n + h->kt_lanes - 1) / h->kt_lanes;
+    hipLaunchKernelGGL(k_traffic, dim3((unsigned)kb), dim3(h->kt_lanes), h->kt_lds, h->stream, h->dcfg, h->dtab, h->S,
+                       h->out, h->tr_slot, h->kt_plan_dw, h->kt_rs_dw);
+    HIPCHK(h, hipGetLastError());
+    if (!h->hcfg.obs_fast && h->hcfg.traffic_ch >= 0) {
+      PgtgOutputs o{};
+      o.obs = h->out.obs;  // only the observation: positions etc. are unchanged
+      hipLaunchKernelGGL(k_env<true>, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
+                         nullptr, nullptr, o, (int)MODE_OBSERVE, h->L, h->tr_slot);
+      HIPCHK(h, hipGetLastError());
+    }
+    h->tr_slot ^= 1u;
+  }
   if (timed) {
     HIPCHK(h, hipEventRecord(h->evpool[h->ev_used + 1], h->stream));
     h->ev_used += 2;
@@ -2097,6 +2236,7 @@ int pgtg_get_env_state(pgtg_handle* h, uint64_t env, PgtgEnvState* st) {
     uint4 t;
     if (int rc = read_traf(h, env, &t)) return rc;
     st->n_cars = (int)(t.x & 0xffffu);
+    st->n_spawners = (int)(t.x >> 16);
     st->next_car_id = (int)t.y;
   }
   return PGTG_OK;

@@ -14,7 +14,7 @@ import torch  # noqa: E402
 
 from pgtg_amd import _abi  # noqa: E402
 
-_abi.LIB_PATH = os.path.join(os.path.dirname(_abi.LIB_PATH), "libpgtg_hip_stamps.so")
+_abi.LIB_PATH = os.environ.get("PGTG_STAMPS_LIB") or os.path.join(os.path.dirname(_abi.LIB_PATH), "libpgtg_hip_stamps.so")
 from pgtg_amd.vector import PGTGVecEnv  # noqa: E402
 
 SLOTS = 32
@@ -48,7 +48,10 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
     lo, hi = st[:, 0], st[:, 6]
     out = {}
     for n, (a, b) in SUB.items():
-        ok = (st[:, a] >= lo) & (st[:, a] <= hi) & (st[:, b] >= st[:, a]) & (st[:, b] <= hi)
+        if n.startswith("traf."):  # k_traffic (after k_env; 64-lane workgroups share the slot rows)
+            ok = (st[:, a] > 0) & (st[:, b] >= st[:, a]) & (st[:, b] - st[:, a] < 1e9)
+        else:
+            ok = (st[:, a] >= lo) & (st[:, a] <= hi) & (st[:, b] >= st[:, a]) & (st[:, b] <= hi)
         if ok.any():
             out[n] = (int((st[ok, b] - st[ok, a]).mean()), round(float(ok.mean()), 2))
     print("  sub-phases (mean cycles, fraction of waves):", out, flush=True)
