@@ -492,29 +492,23 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
                                              Pcg& cr, uint8_t* rs, TrafState& ts, int at, uint32_t* CR) {
   const uint64_t N = S.n;
   STAMP(19);
-  // car spawners in x-major order -> HBM list
-  int nsp = 0;
+  // one x-major sweep: car spawners -> HBM list, spawnable squares (any car lane) -> per-column
+  // prefix counts
+  uint16_t* colpre = reinterpret_cast<uint16_t*>(rs + c.rs_pre_off);
+  int nsp = 0, np = 0;
   for (int x = 0; x < c.W; x++) {
-    int tx = x / kTile, lx = x - tx * kTile;
+    const int tx = x / kTile, lx = x - tx * kTile;
+    colpre[x] = (uint16_t)np;
     for (int ty = 0; ty < c.th; ty++) {
-      uint32_t m = spawner_colmask(c, plan_exits(pl[ty * c.tw + tx]), tx, ty, lx);
+      const uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
+      np += __popc(sT.lanecol[ex][lx]);  // row 0 (no exits) is empty
+      uint32_t m = spawner_colmask(c, ex, tx, ty, lx);
       while (m) {
         int ly = __ffs((int)m) - 1;
         m &= m - 1u;
         if (nsp < c.max_spawners) S.spawners[(uint64_t)nsp * N + i] = (uint16_t)(x | (ty * kTile + ly) << 8);
         nsp++;
       }
-    }
-  }
-  // spawnable positions (squares holding any car lane), x-major: per-column prefix counts
-  uint16_t* colpre = reinterpret_cast<uint16_t*>(rs + c.rs_pre_off);
-  int np = 0;
-  for (int x = 0; x < c.W; x++) {
-    int tx = x / kTile, lx = x - tx * kTile;
-    colpre[x] = (uint16_t)np;
-    for (int ty = 0; ty < c.th; ty++) {
-      uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
-      if (ex) np += __popc(sT.lanecol[ex][lx]);
     }
   }
   colpre[c.W] = (uint16_t)np;
@@ -538,41 +532,48 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
     STAMP(21);
     for (int m = k - 1; m >= 1; m--) {
       int jj = (int)pcg_int(cr, (uint32_t)(m + 1));
-      uint16_t t = out[m];
-      out[m] = out[jj];
+      const uint16_t t = out[m], u = out[jj];
+      out[m] = u;
       out[jj] = t;
     }
     STAMP(22);
+    const int tw = c.tw, th = c.th;
     for (int m = 0; m < k; m++) {
-      int idx = out[m];
-      // x: last column whose prefix <= idx
-      int lo = 0, hi = c.W;  // colpre[lo] <= idx < colpre[hi]
-      while (hi - lo > 1) {
-        int mid = (lo + hi) >> 1;
-        if (colpre[mid] <= idx) lo = mid; else hi = mid;
-      }
-      int x = lo, rr = idx - colpre[x], tx = x / kTile, lx = x - tx * kTile, y = 0, t_car = -1, ly = 0;
-      for (int ty = 0; ty < c.th; ty++) {
-        uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
-        uint32_t msk = ex ? sT.lanecol[ex][lx] : 0u;
-        int cnt = __popc(msk);
-        if (rr < cnt) {
-          ly = kth_bit(msk, rr);
-          y = ty * kTile + ly;
-          t_car = ty * c.tw + tx;
-          break;
+      const int idx = out[m];
+      // column: the tile column from the prefixes at tile-column starts, then the column inside it
+      int tx = 0;
+      for (int q = 1; q < tw; q++) tx += colpre[q * kTile] <= idx ? 1 : 0;
+      const uint16_t* cp = colpre + tx * kTile;
+      int lx = 0;
+#pragma unroll
+      for (int j = 1; j < kTile; j++) lx += cp[j] <= idx ? 1 : 0;
+      // row: the tile of the column holding the rr-th spawnable square (no early exit)
+      int rr = idx - cp[lx], ty_f = 0, rr_f = 0;
+      uint32_t ex_f = 0, msk_f = 0;
+      for (int ty = 0; ty < th; ty++) {
+        const uint32_t ex = plan_exits(pl[ty * tw + tx]);
+        const uint32_t msk = sT.lanecol[ex][lx];
+        const int cnt = __popc(msk);
+        if (rr >= 0 && rr < cnt) {
+          ty_f = ty;
+          ex_f = ex;
+          msk_f = msk;
+          rr_f = rr;
         }
         rr -= cnt;
       }
-      if (t_car == at) {
-        const int sq = lx * 9 + ly;
-        CR[sq >> 5] |= 1u << (sq & 31);
-      }
-      uint32_t rl = square_lanes(c, pl, x, y) & 0x0fffffffu;
-      int nr = __popc(rl);
+      const int ly = kth_bit(msk_f, rr_f);
+      const int x = tx * kTile + lx, y = ty_f * kTile + ly, sq = lx * 9 + ly;
+      if (ty_f * tw + tx == at) CR[sq >> 5] |= 1u << (sq & 31);
+      const uint32_t rl = sT.lanes[ex_f][sq] & 0x0fffffffu;
+      const uint32_t nr = __popc(rl);
       if (nr == 0) return PGTG_E_MAP;  // "a car was spawned on a field where no car lane was found"
-      int prof = pcg_choice_cdf<5>(cr, c.profile_t);
-      int route = sT.lane_route[kth_bit(rl, (int)pcg_int(cr, (uint32_t)nr))];
+      const uint64_t u = pcg_draw(cr, false, 0u);
+      int prof = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) prof += (u < c.profile_t[j]) ? 0 : 1;
+      const uint32_t rk = nr > 1u ? (uint32_t)pcg_draw(cr, true, nr) : 0u;
+      const int route = sT.lane_route[kth_bit(rl, (int)rk)];
       uint64_t a = cs.at(0, c.car_cap, m);
       cs.w0[a] = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
       cs.w1[a] = 0u;
