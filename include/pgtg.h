@@ -12,6 +12,7 @@
  *   pgtg_get_cars / pgtg_get_env_state <- get_info() fields             environment.py:1538-1578
  *   pgtg_set_agent / pgtg_add_car      <- test-style state overrides (env.position = ..., env.cars.append)
  *   pgtg_get_map_plan <- EpisodeMap.map_plan / save_map                 pgtg/map.py:173-184
+ *   pgtg_get_squares  <- EpisodeMap.squares feature sets (feature_at)   pgtg/map.py:49-69, parser.py:13-166
  *   pgtg_get_counters <- (new) device-side env-step / episode counters
  *
  * Conventions: all pointers named *_dev are device pointers (hipMalloc'd or torch data_ptr) on the
@@ -125,7 +126,8 @@ typedef struct {
   int32_t* final_position; /* [N][2] */
   int32_t* final_velocity; /* [N][2] */
   int32_t* final_next_subgoal; /* [N] */
-  uint8_t* braking;        /* [N] info['traffic_rules']['braking_applied'] */
+  uint8_t* braking;        /* [N] triggered traffic rules, bit r = PgtgConfig.rules[r] (rule_triggers);
+                              nonzero <=> info['traffic_rules']['braking_applied'] */
 } PgtgOutputs;
 
 typedef struct {
@@ -162,8 +164,24 @@ int pgtg_get_env_state(pgtg_handle* h, uint64_t env, PgtgEnvState* st);
 int pgtg_get_cars(pgtg_handle* h, uint64_t env, PgtgCar* cars, int32_t cap, int32_t* n);
 int pgtg_get_map_plan(pgtg_handle* h, uint64_t env, int32_t* w, int32_t* h_, uint8_t* exits, int8_t* otype,
                       int8_t* omask, int32_t* start3, int32_t* goal3);
+/* The episode map's squares as feature words, x-major (index x * height + y), height = 9 * tile rows:
+ * bits 0-31 the car lanes (lane ids of the tables), then the PGTG_SQ_* flags below. */
+#define PGTG_SQ_WALL (1ull << 32)
+#define PGTG_SQ_SPAWNER (1ull << 37)
+#define PGTG_SQ_START (1ull << 38)
+#define PGTG_SQ_SUBGOAL (1ull << 39)
+#define PGTG_SQ_USED_SUBGOAL (1ull << 40)
+#define PGTG_SQ_FINAL_GOAL (1ull << 41)
+#define PGTG_SQ_ICE (1ull << 42)
+#define PGTG_SQ_BROKEN_ROAD (1ull << 43)
+#define PGTG_SQ_SAND (1ull << 44)
+#define PGTG_SQ_TRAFFIC_LIGHT (1ull << 45)
+int pgtg_get_squares(pgtg_handle* h, uint64_t env, uint64_t* words, int32_t cap, int32_t* width, int32_t* height);
 int pgtg_set_agent(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t vx, int32_t vy);
 int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t route, int32_t profile);
+/* Replace the traffic rules of every env (add_traffic_rule / remove_traffic_rule,
+ * environment.py:569-575); takes effect from the next step.  n_rules <= PGTG_MAX_RULES. */
+int pgtg_set_rules(pgtg_handle* h, const PgtgRule* rules, int32_t n_rules);
 /* Re-emit the observation of every env into the bound outputs (after set_agent/add_car). */
 int pgtg_observe(pgtg_handle* h);
 /* steps (env-steps executed) and episodes (resets) since create, summed over envs; synchronises. */

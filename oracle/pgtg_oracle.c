@@ -1017,7 +1017,7 @@ static int apply_braking(orc_env* e) {
     for (int i = 0; i < e->ncars; i++)
       if (e->cars[i].x / TILE == tx && e->cars[i].y / TILE == ty) match += r->weight[dir][e->cars[i].route];
     if (match < r->min_matching_traffic) continue;
-    triggered = 1;
+    triggered |= 1 << ri; /* rule_triggers: every rule is evaluated */
   }
   return triggered;
 }

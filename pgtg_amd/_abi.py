@@ -28,7 +28,7 @@ PGTG_E_MAP = -5
 EXPORTED = [
     "pgtg_create", "pgtg_destroy", "pgtg_set_stream", "pgtg_set_outputs", "pgtg_reset",
     "pgtg_reset_unseeded", "pgtg_step", "pgtg_random_actions", "pgtg_get_env_state", "pgtg_get_cars",
-    "pgtg_get_map_plan", "pgtg_set_agent", "pgtg_add_car", "pgtg_observe", "pgtg_get_counters",
+    "pgtg_get_map_plan", "pgtg_get_squares", "pgtg_set_rules", "pgtg_set_agent", "pgtg_add_car", "pgtg_observe", "pgtg_get_counters",
     "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_launch_info", "pgtg_last_error", "pgtg_enable_timing",
     "pgtg_timing_read",
 ]
@@ -111,6 +111,8 @@ def lib():
         "pgtg_get_env_state": ([vp, u64, C.POINTER(PgtgEnvState)], C.c_int),
         "pgtg_get_cars": ([vp, u64, C.POINTER(PgtgCar), i32, C.POINTER(i32)], C.c_int),
         "pgtg_get_map_plan": ([vp, u64] + [vp] * 7, C.c_int),
+        "pgtg_get_squares": ([vp, u64, vp, i32, C.POINTER(i32), C.POINTER(i32)], C.c_int),
+        "pgtg_set_rules": ([vp, vp, i32], C.c_int),
         "pgtg_set_agent": ([vp, u64, i32, i32, i32, i32], C.c_int),
         "pgtg_add_car": ([vp, u64, i32, i32, i32, i32], C.c_int),
         "pgtg_observe": ([vp], C.c_int),
@@ -129,6 +131,20 @@ def lib():
         f.restype = res
     _lib = L
     return L
+
+
+def fill_rules(dst, rules) -> int:
+    """Compiled traffic rules (config.CompiledRule) into a PgtgRule array; returns the count."""
+    if len(rules) > MAX_RULES:
+        raise ValueError(f"at most {MAX_RULES} traffic rules are supported")
+    for i, r in enumerate(rules):
+        o = dst[i]
+        o.tile_exits, o.speed_sq_min, o.speed_sq_max = r.tile_exits, r.speed_sq_min, r.speed_sq_max
+        o.min_traffic, o.min_matching_traffic = r.min_traffic, r.min_matching_traffic
+        for d in range(6):
+            for k in range(20):
+                o.weight[d][k] = r.weight[d][k]
+    return len(rules)
 
 
 def config_struct(spec: "cfgmod.EnvSpec", autoreset: bool, max_episode_steps: int | None,
@@ -163,14 +179,7 @@ def config_struct(spec: "cfgmod.EnvSpec", autoreset: bool, max_episode_steps: in
     for i in range(5):
         c.profile_pct[i] = float(spec.profile_pct[i])
     c.separate_reward_cost = int(spec.separate_reward_cost)
-    c.n_rules = len(spec.rules)
-    for i, r in enumerate(spec.rules):
-        o = c.rules[i]
-        o.tile_exits, o.speed_sq_min, o.speed_sq_max = r.tile_exits, r.speed_sq_min, r.speed_sq_max
-        o.min_traffic, o.min_matching_traffic = r.min_traffic, r.min_matching_traffic
-        for d in range(6):
-            for k in range(20):
-                o.weight[d][k] = r.weight[d][k]
+    c.n_rules = fill_rules(c.rules, spec.rules)
     fm = spec.fixed_map
     if fm is not None:
         if fm.width * fm.height > MAX_TILES:

@@ -1043,9 +1043,10 @@ __device__ __forceinline__ BrakeQuery braking_query(const DevCfg& c, const EnvVi
   if (q.cand) q.tile = ty * c.tw + tx;
   return q;
 }
-__device__ __forceinline__ bool braking_decide(const DevCfg& c, const DevState& S, const EnvView& v, const Plan& pl,
-                                               const BrakeQuery& q, const uint8_t* hist) {
-  if (!q.cand) return false;
+// returns the mask of triggered rules (TrafficRuleEngine.evaluate_all_rules, rule_triggers)
+__device__ __forceinline__ uint32_t braking_decide(const DevCfg& c, const DevState& S, const EnvView& v,
+                                                   const Plan& pl, const BrakeQuery& q, const uint8_t* hist) {
+  if (!q.cand) return 0u;
   // agent direction from the subgoal compass (environment.py:185-206, 1037-1090)
   int dir;
   int bx = 0, by = 0;
@@ -1054,18 +1055,20 @@ __device__ __forceinline__ bool braking_decide(const DevCfg& c, const DevState& 
     cp = S.cmp_tab[(bx - v.px + c.cmp_off) * c.cmp_pitch + (by - v.py + c.cmp_off)];
   if (cp >= 0) dir = cp >> 1;  // N,NE -> south_to_north; E,SE -> west_to_east; S,SW; W,NW
   else dir = q.s2 == 0 ? 4 : 5;  // "stationary" (speed < 0.1) / "near_goal"
+  uint32_t trig = 0u;
   for (int r = 0; r < c.n_rules; r++) {
     if (!((q.cand >> r) & 1u)) continue;
     if (q.n_in < c.rules[r].min_traffic) continue;
     int match = 0;
     for (int k = 0; k < 20; k++) match += hist[k] * (int)sT.rule_w[r][dir][k];
-    if (match >= c.rules[r].min_matching_traffic) return true;
+    if (match >= c.rules[r].min_matching_traffic) trig |= 1u << r;
   }
-  return false;
+  return trig;
 }
 
 struct StepResult {
   double reward, cost;
+  uint32_t triggered;  // traffic rules that triggered braking (bit r = rule r)
 };
 
 template <bool TR>
@@ -1098,7 +1101,8 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
   v.vx += ax;
   v.vy += ay;
   v.flags &= ~kFlagBraking;
-  if (TR && c.n_rules > 0 && braking_decide(c, S, v, pl, bq, hist)) {  // environment.py:1145
+  res.triggered = (TR && c.n_rules > 0) ? braking_decide(c, S, v, pl, bq, hist) : 0u;
+  if (res.triggered) {  // environment.py:1145
     v.vx = v.vy = 0;
     v.flags |= kFlagBraking;
   }
@@ -1445,14 +1449,14 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   uint8_t my_sel = 0;
   if (live) {
     if (mode == MODE_STEP) {
-      StepResult res{0.0, 0.0};
+      StepResult res{0.0, 0.0, 0u};
       if (!err) err = env_step<TR>(c, S, i, v, pl, actions[i], res, occ, sp_l, ts, hist);
       const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
       if (out.reward) out.reward[i] = res.reward;
       if (out.cost) out.cost[i] = res.cost;
       if (out.terminated) out.terminated[i] = (v.flags & kFlagTerminated) ? 1 : 0;
       if (out.truncated) out.truncated[i] = (v.flags & kFlagTruncated) ? 1 : 0;
-      if (out.braking) out.braking[i] = (v.flags & kFlagBraking) ? 1 : 0;
+      if (out.braking) out.braking[i] = (uint8_t)res.triggered;
       my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
     } else if (mode == MODE_RESET_SEEDED || mode == MODE_RESET_UNSEEDED) {
       const bool do_reset = mask == nullptr || mask[i] != 0;
@@ -1585,6 +1589,39 @@ __global__ void __launch_bounds__(64) k_traffic(const DevCfg* __restrict__ cfg, 
         o[k * 32 + b] = 1;
       }
     }
+  }
+}
+
+// Feature words of every square of env i's map (introspection: get_info, tests); one workgroup.
+__global__ void __launch_bounds__(kBlock) k_squares(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
+                                                    DevState S, uint64_t i, uint64_t* __restrict__ words) {
+  __shared__ uint16_t plan_s[kMaxTiles];
+  const DevCfg& c = *cfg;
+  const int tid = threadIdx.x;
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
+    uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
+    for (int k = tid; k < (int)(sizeof(Tables) / 4); k += blockDim.x) dstt[k] = src[k];
+    for (int t = tid; t < c.nt; t += blockDim.x) plan_s[t] = S.plan[i * (uint64_t)c.plan_stride + t];
+  }
+  __syncthreads();
+  const EnvView v = rec_load(S.rec, i);
+  const Plan pl{plan_s};
+  for (int q = tid; q < c.W * c.H; q += blockDim.x) {
+    const int x = q / c.H, y = q - x * c.H;
+    const uint32_t f = square_flags(c, pl, v, x, y);
+    uint64_t w = square_lanes(c, pl, x, y);
+    if (f & SQ_WALL) w |= 1ull << 32;
+    if (square_spawner(c, pl, x, y)) w |= 1ull << 37;
+    if (f & SQ_START) w |= 1ull << 38;
+    if (f & SQ_SUBGOAL) w |= 1ull << 39;
+    if (f & SQ_USED) w |= 1ull << 40;
+    if (f & SQ_FINAL) w |= 1ull << 41;
+    if (f & SQ_ICE) w |= 1ull << 42;
+    if (f & SQ_BROKEN) w |= 1ull << 43;
+    if (f & SQ_SAND) w |= 1ull << 44;
+    if (f & SQ_TLIGHT) w |= 1ull << 45;
+    words[q] = w;
   }
 }
 
@@ -2296,6 +2333,44 @@ int pgtg_get_map_plan(pgtg_handle* h, uint64_t env, int32_t* w, int32_t* h_, uin
   goal3[0] = (int)((sg >> 16) & 0xffu) % c.tw;
   goal3[1] = (int)((sg >> 16) & 0xffu) / c.tw;
   goal3[2] = (int)(sg >> 24);
+  return PGTG_OK;
+}
+
+int pgtg_get_squares(pgtg_handle* h, uint64_t env, uint64_t* words, int32_t cap, int32_t* width, int32_t* height) {
+  if (!h || env >= h->n) return PGTG_E_INVALID;
+  const DevCfg& c = h->hcfg;
+  if (width) *width = c.W;
+  if (height) *height = c.H;
+  if (!words) return PGTG_OK;
+  if (cap < c.W * c.H) return fail(h, PGTG_E_INVALID, "squares buffer too small");
+  HIPCHK(h, hipSetDevice(h->device));
+  uint64_t* d = nullptr;
+  HIPCHK(h, hipMalloc(&d, (size_t)c.W * c.H * 8));
+  hipLaunchKernelGGL(k_squares, dim3(1), dim3(kBlock), 0, h->stream, h->dcfg, h->dtab, h->S, env, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e == hipSuccess) e = hipMemcpy(words, d, (size_t)c.W * c.H * 8, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(h, PGTG_E_DEVICE, std::string("pgtg_get_squares: ") + hipGetErrorString(e));
+  return PGTG_OK;
+}
+
+int pgtg_set_rules(pgtg_handle* h, const PgtgRule* rules, int32_t n_rules) {
+  if (!h || n_rules < 0 || n_rules > PGTG_MAX_RULES || (n_rules > 0 && !rules))
+    return h ? fail(h, PGTG_E_INVALID, "bad rule count") : PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  DevCfg& c = h->hcfg;
+  bool possible = c.need_car;
+  for (int k = 0; k < n_rules; k++) {
+    c.rules[k] = rules[k];
+    possible = possible || rules[k].min_traffic <= 0;
+  }
+  c.n_rules = possible ? n_rules : 0;
+  uint8_t w[PGTG_MAX_RULES][6][20] = {};
+  for (int k = 0; k < n_rules; k++) memcpy(w[k], rules[k].weight, sizeof w[k]);
+  HIPCHK(h, hipMemcpy(h->dcfg, &c, sizeof(DevCfg), hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(reinterpret_cast<uint8_t*>(h->dtab) + offsetof(Tables, rule_w), w, sizeof w, hipMemcpyHostToDevice));
   return PGTG_OK;
 }
 

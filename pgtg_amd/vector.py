@@ -64,7 +64,7 @@ class PGTGVecEnv:
         self.reward = t.zeros((N,), dtype=t.float64, device=dev)
         self.terminated = t.zeros((N,), dtype=t.bool, device=dev)
         self.truncated = t.zeros((N,), dtype=t.bool, device=dev)
-        self.braking = t.zeros((N,), dtype=t.bool, device=dev)
+        self.braking = t.zeros((N,), dtype=t.uint8, device=dev)  # triggered-rule mask
         self.cost = t.zeros((N,), dtype=t.float64, device=dev) if self.spec.separate_reward_cost else None
         self.nsd = t.full((N,), -1, dtype=t.int32, device=dev) if self.spec.next_subgoal else None
         if autoreset:
@@ -156,7 +156,7 @@ class PGTGVecEnv:
         _check(self._lib.pgtg_step(self._h, C.c_void_p(a.data_ptr())), self._h)
         if not self.autoreset:
             self._raise_errors()
-        infos: dict[str, Any] = {"braking_applied": self.braking}
+        infos: dict[str, Any] = {"braking_applied": self.braking != 0, "triggered_rules_mask": self.braking}
         if self.autoreset:
             done = self.terminated | self.truncated
             infos["final_observation"] = self.final_observation()
@@ -213,6 +213,37 @@ class PGTGVecEnv:
         n = w.value * h.value
         return {"w": w.value, "h": h.value, "exits": list(ex[:n]), "otype": list(ot[:n]), "omask": list(om[:n]),
                 "start": tuple(s3), "goal": tuple(g3)}
+
+    def squares(self, i: int):
+        """Feature words of env i's map squares, numpy uint64 [W*9][H*9] (include/pgtg.h PGTG_SQ_*)."""
+        import numpy as np
+        w, h = C.c_int32(), C.c_int32()
+        _check(self._lib.pgtg_get_squares(self._h, i, None, 0, C.byref(w), C.byref(h)), self._h)
+        out = np.zeros(w.value * h.value, np.uint64)
+        _check(self._lib.pgtg_get_squares(self._h, i, C.c_void_p(out.ctypes.data), out.size, C.byref(w),
+                                          C.byref(h)), self._h)
+        return out.reshape(w.value, h.value)
+
+    # -- traffic rules (TrafficRuleEngine via PGTGEnv.add_traffic_rule / remove_traffic_rule) ---------
+    def _push_rules(self):
+        arr = (_abi.PgtgRule * _abi.MAX_RULES)()
+        n = _abi.fill_rules(arr, self.spec.rules)
+        _check(self._lib.pgtg_set_rules(self._h, arr, n), self._h)
+
+    def add_traffic_rule(self, rule_dict: dict):
+        from .config import add_rule
+        add_rule(self.spec, rule_dict)
+        self._push_rules()
+
+    def remove_traffic_rule(self, rule_name: str) -> bool:
+        from .config import remove_rule
+        removed = remove_rule(self.spec, rule_name)
+        if removed:
+            self._push_rules()
+        return removed
+
+    def rule_names(self) -> list[str]:
+        return [r.name for r in self.spec.rules]
 
     def set_agent(self, i: int, x: int, y: int, vx: int, vy: int):
         _check(self._lib.pgtg_set_agent(self._h, i, x, y, vx, vy), self._h)

@@ -83,7 +83,7 @@ def replay_oracle(d: dict, n_envs: int | None = None, steps: int | None = None) 
                 bad.append(f"{tag} terminated")
             if spec.next_subgoal and r["nsd"] != d["nsd"][t, i]:
                 bad.append(f"{tag} nsd {r['nsd']} vs {d['nsd'][t, i]}")
-            if r["braking"] != d["braking"][t, i]:
+            if bool(r["braking"]) != bool(d["braking"][t, i]):
                 bad.append(f"{tag} braking")
             if digest(env.cars()) != int(d["cars_dig"][t, i]):
                 bad.append(f"{tag} cars")
@@ -141,6 +141,7 @@ def replay_vec(d: dict, n_envs: int | None = None, steps: int | None = None) -> 
         rew, term = env.reward.cpu().numpy(), env.terminated.cpu().numpy()
         trunc = env.truncated.cpu().numpy()
         cost = env.cost.cpu().numpy() if env.cost is not None else np.zeros(N)
+        brk = env.braking.cpu().numpy()
         nsd = env.nsd.cpu().numpy() if env.nsd is not None else None
         fnsd = env.final_nsd.cpu().numpy() if env.final_nsd is not None else None
         check_cars = has_traffic(meta)
@@ -154,6 +155,8 @@ def replay_vec(d: dict, n_envs: int | None = None, steps: int | None = None) -> 
             if bool(term[i]) != bool(d["terminated"][t, i]) or trunc[i]:
                 bad.append(f"{tag} terminated {term[i]} vs {d['terminated'][t, i]}")
                 continue
+            if bool(brk[i]) != bool(d["braking"][t, i]):
+                bad.append(f"{tag} braking {brk[i]} vs {d['braking'][t, i]}")
             if rew[i] != d["reward"][t, i] or cost[i] != d["cost"][t, i]:
                 bad.append(f"{tag} reward {rew[i]} vs {d['reward'][t, i]} cost {cost[i]} vs {d['cost'][t, i]}")
             if term[i]:

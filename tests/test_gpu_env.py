@@ -1,0 +1,182 @@
+"""The single-env facade (pgtg_amd.env.PGTGEnv, the reference's PGTGEnv surface) and the
+introspection / rule entry points of the C ABI, against the CPU oracle on the same seeds."""
+import copy
+import warnings
+
+import numpy as np
+import pytest
+
+import helpers  # noqa: F401  (sys.path)
+from oracle.oracle import OracleEnv
+from pgtg_amd import config as cfg
+
+pytestmark = pytest.mark.gpu
+
+F_EXITS = np.uint64(0xF << 33)  # the oracle keeps exit markers in its square words; the ABI does not
+
+
+def _spec(**kw):
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        return cfg.make_spec(**kw)
+
+
+def _env(**kw):
+    from pgtg_amd.env import PGTGEnv
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        return PGTGEnv(**kw)
+
+
+def _cmp_obs(env, obs, r, where):
+    keys = [k for k, _ in env.spec.channels]
+    for c, k in enumerate(keys):
+        assert np.array_equal(obs["map"][k], r["obs"][c].astype(np.int64)), f"{where}: channel {k}"
+    assert tuple(obs["position"]) == tuple(r["pos"]), where
+    assert tuple(obs["velocity"]) == tuple(r["vel"]), where
+    if env.spec.next_subgoal:
+        assert obs["next_subgoal_direction"] == r["nsd"], where
+
+
+KW = dict(random_map_width=4, random_map_height=4, traffic_density=0.3, random_map_obstacle_probability=0.4,
+          use_next_subgoal_direction=True)
+
+
+def test_facade_episode_matches_oracle():
+    env = _env(**KW)
+    orc = OracleEnv(env.spec)
+    rng = np.random.default_rng(3)
+    obs, info = env.reset(seed=11)
+    r = orc.reset(11)
+    _cmp_obs(env, obs, r, "reset")
+    assert info["traffic_rules"]["active_rules"] == [x.name for x in env.spec.rules]
+    episodes = 0
+    for t in range(120):
+        a = int(rng.integers(0, 9))
+        obs, rew, term, trunc, info = env.step(a)
+        r = orc.step(a)
+        _cmp_obs(env, obs, r, f"t{t}")
+        assert rew == r["reward"] and term == r["terminated"] and trunc is False
+        assert info["traffic_rules"]["braking_applied"] == bool(r["braking"])
+        names = [x.name for k, x in enumerate(env.spec.rules) if (r["braking"] >> k) & 1]
+        assert info["traffic_rules"]["triggered_rules"] == names
+        cars = orc.cars()
+        assert [(c["id"], c["x"], c["y"], c["patience_counter"]) for c in info["cars"]] == \
+            [(int(c[0]), int(c[1]), int(c[2]), int(c[5])) for c in cars]
+        assert [c["route"] for c in info["cars"]] == [cfg.ROUTES[int(c[3])] for c in cars]
+        assert info["driver_profile_stats"]["total_cars"] == len(cars)
+        W, H = env.squares().shape
+        if 0 <= info["x"] < W and 0 <= info["y"] < H:  # obs position = offset inside the agent's tile
+            assert (info["x"] % 9, info["y"] % 9) == tuple(r["pos"])
+        if term:
+            with pytest.raises(RuntimeError, match="Already done"):
+                env.step(0)
+            assert env.applicable_actions() == []
+            obs, info = env.reset()
+            r = orc.reset(None)
+            _cmp_obs(env, obs, r, f"t{t} reset")
+            episodes += 1
+    assert episodes > 0
+    env.close()
+
+
+def test_tile_type_and_squares_match_oracle():
+    env = _env(**KW)
+    orc = OracleEnv(env.spec)
+    for seed in (0, 5, 9):
+        obs, info = env.reset(seed=seed)
+        orc.reset(seed)
+        sq = env.squares().reshape(-1)
+        want = orc.squares() & ~F_EXITS
+        assert np.array_equal(sq, want), f"seed {seed}: {int((sq != want).sum())} squares differ"
+        plan = orc.map_plan()
+        x, y = info["x"], info["y"]
+        tx, ty = min(max(x // 9, 0), plan["w"] - 1), min(max(y // 9, 0), plan["h"] - 1)
+        ex = plan["exits"][ty * plan["w"] + tx]
+        assert info["current_tile_type"] == "".join(str((ex >> d) & 1) for d in range(4))
+    env.close()
+
+
+def test_position_setter_then_step_matches_oracle():
+    env = _env(random_map_width=3, random_map_height=3)
+    orc = OracleEnv(env.spec)
+    env.reset(seed=2)
+    orc.reset(2)
+    x, y = (int(v) for v in env.position)
+    env.position = (x + 1, y)
+    orc.set_agent(x + 1, y)
+    assert tuple(env.position) == (x + 1, y)
+    for a in (5, 7, 4):
+        obs, rew, term, _, _ = env.step(a)
+        r = orc.step(a)
+        _cmp_obs(env, obs, r, f"action {a}")
+        assert rew == r["reward"] and term == r["terminated"]
+        if term:
+            break
+    env.close()
+
+
+def test_removed_rule_matches_oracle_without_it():
+    kw = dict(random_map_width=5, random_map_height=5, traffic_density=0.5)
+    env = _env(**kw)
+    assert env.remove_traffic_rule("four_way_intersection_brake")
+    assert not env.remove_traffic_rule("no_such_rule")
+    spec = copy.deepcopy(env.spec)
+    orc = OracleEnv(spec)
+    rng = np.random.default_rng(8)
+    env.reset(seed=4)
+    orc.reset(4)
+    fired = 0
+    for t in range(80):
+        a = int(rng.integers(0, 9))
+        obs, rew, term, _, info = env.step(a)
+        r = orc.step(a)
+        _cmp_obs(env, obs, r, f"t{t}")
+        assert info["traffic_rules"]["braking_applied"] == bool(r["braking"])
+        fired += bool(r["braking"])
+        if term:
+            env.reset()
+            orc.reset(None)
+    assert "four_way_intersection_brake" not in env.get_info()["traffic_rules"]["active_rules"]
+    env.add_traffic_rule(cfg.DEFAULT_RULES[0])
+    with pytest.raises(ValueError):
+        env.add_traffic_rule(cfg.DEFAULT_RULES[0])
+    env.close()
+
+
+def test_triggered_mask_over_golden_braking_trajectory():
+    """The vector env's per-env triggered-rule mask equals the oracle's on a traffic-heavy batch."""
+    import torch
+    from pgtg_amd.vector import PGTGVecEnv
+    spec = _spec(random_map_width=5, random_map_height=5, traffic_density=0.5)
+    N, T = 16, 30
+    vec = PGTGVecEnv(N, spec=spec, autoreset=False)
+    vec.reset(seed=100)
+    orcs = [OracleEnv(spec) for _ in range(N)]
+    for i, o in enumerate(orcs):
+        o.reset(100 + i)
+    rng = np.random.default_rng(1)
+    done = np.zeros(N, bool)
+    hits = 0
+    for t in range(T):
+        acts = rng.integers(0, 9, N).astype(np.uint8)
+        acts[done] = 0
+        if done.all():
+            break
+        # finished envs are reset on the host side of the test, like a non-autoreset caller would
+        if done.any():
+            vec.reset(mask=torch.as_tensor(done), seed=None)
+            for i in np.nonzero(done)[0]:
+                orcs[i].reset(None)
+            done[:] = False
+        vec.step(torch.as_tensor(acts))
+        torch.cuda.synchronize()
+        mask = vec.braking.cpu().numpy()
+        term = vec.terminated.cpu().numpy()
+        for i in range(N):
+            r = orcs[i].step(int(acts[i]))
+            assert int(mask[i]) == int(r["braking"]), f"env {i} t {t}"
+            hits += int(mask[i] != 0)
+            done[i] = bool(term[i])
+    assert hits > 0
+    vec.close()
