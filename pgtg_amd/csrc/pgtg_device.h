@@ -99,7 +99,9 @@ struct Tables {
   uint32_t obst[14][3];     // kObstMask
   uint32_t spawner[16][3];  // kLaneSpawner
   double ind[kMaxTiles + 1];  // sum_subgoals_reward / num_subgoals
-  uint8_t ea[kMaxEdges], eb[kMaxEdges], ed[kMaxEdges], erev[kMaxEdges];
+  // removable edges in graph-theory order, oriented: a | b<<8 | d<<16 | reverse edge<<24 with a the
+  // north/west tile and d 1 (east) or 2 (south)
+  uint32_t epk[kMaxEdges];
   uint8_t bt[kMaxBorder], bd[kMaxBorder];
   uint32_t lanes[16][81];   // kLanes (copied only when traffic or lane/spawner channels need it)
   // traffic tables (copied with lanes): lane-square slot per square (255 = none), square per slot,

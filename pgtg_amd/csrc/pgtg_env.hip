@@ -220,42 +220,54 @@ __device__ __forceinline__ int rand_dir(const DevCfg& c, Pcg& r, int x, int y) {
 }
 
 // 256-bit set kept in four named registers (no private-array indexing -> no scratch)
-struct Bits256 {
-  uint64_t w0, w1, w2, w3;
+// k-th (0-based) set bit of a 64-bit word, branch-free (popcount halving)
+__device__ __forceinline__ int select64(uint64_t x, int k) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const int cl = __popc(lo);
+  bool up = k >= cl;
+  uint32_t y = up ? hi : lo;
+  int base = up ? 32 : 0;
+  k -= up ? cl : 0;
+#pragma unroll
+  for (int half = 16; half >= 1; half >>= 1) {
+    const int cnt = __popc(y & ((1u << half) - 1u));
+    up = k >= cnt;
+    y = up ? y >> half : y;
+    base += up ? half : 0;
+    k -= up ? cnt : 0;
+  }
+  return base;
+}
+
+// NW x 64 edge bits (the reference's shrinking removable_edges list as a membership set)
+template <int NW>
+struct EdgeBits {
+  uint64_t w[NW];
   __device__ __forceinline__ void init(int n) {
-    w0 = n >= 64 ? ~0ull : (n <= 0 ? 0ull : ((1ull << n) - 1ull));
-    w1 = n >= 128 ? ~0ull : (n <= 64 ? 0ull : ((1ull << (n - 64)) - 1ull));
-    w2 = n >= 192 ? ~0ull : (n <= 128 ? 0ull : ((1ull << (n - 128)) - 1ull));
-    w3 = n >= 256 ? ~0ull : (n <= 192 ? 0ull : ((1ull << (n - 192)) - 1ull));
+#pragma unroll
+    for (int q = 0; q < NW; q++) {
+      const int m = n - 64 * q;
+      w[q] = m >= 64 ? ~0ull : (m <= 0 ? 0ull : ((1ull << m) - 1ull));
+    }
   }
   __device__ __forceinline__ void clear(int i) {
-    uint64_t m = ~(1ull << (i & 63));
-    int q = i >> 6;
-    w0 &= q == 0 ? m : ~0ull;
-    w1 &= q == 1 ? m : ~0ull;
-    w2 &= q == 2 ? m : ~0ull;
-    w3 &= q == 3 ? m : ~0ull;
+#pragma unroll
+    for (int q = 0; q < NW; q++) w[q] &= (i >> 6) == q ? ~(1ull << (i & 63)) : ~0ull;
   }
-  // index of the k-th (0-based) set bit
   __device__ __forceinline__ int select(int k) const {
-    int c0 = __popcll(w0), c1 = __popcll(w1), c2 = __popcll(w2);
-    uint64_t x;
-    int base;
-    if (k < c0) { x = w0; base = 0; }
-    else if (k < c0 + c1) { x = w1; base = 64; k -= c0; }
-    else if (k < c0 + c1 + c2) { x = w2; base = 128; k -= c0 + c1; }
-    else { x = w3; base = 192; k -= c0 + c1 + c2; }
-    // k-th set bit of x by halving with popcounts
-    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-    int cl = __popc(lo);
-    uint32_t y = k < cl ? lo : hi;
-    if (k >= cl) { base += 32; k -= cl; }
-    int c16 = __popc(y & 0xffffu);
-    if (k >= c16) { y >>= 16; base += 16; k -= c16; }
-    int c8 = __popc(y & 0xffu);
-    if (k >= c8) { y >>= 8; base += 8; k -= c8; }
-    for (int j = 0; j < k; j++) y &= y - 1u;
-    return base + __ffs((int)y) - 1;
+    uint64_t x = w[0];
+    int base = 0;
+    bool go = true;
+#pragma unroll
+    for (int q = 0; q + 1 < NW; q++) {  // walk the words with uniform control flow
+      const int cnt = __popcll(x);
+      const bool next = go && k >= cnt;
+      k -= next ? cnt : 0;
+      base += next ? 64 : 0;
+      x = next ? w[q + 1] : x;
+      go = next;
+    }
+    return base + select64(x, k);
   }
 };
 
@@ -287,38 +299,34 @@ __device__ __forceinline__ bool still_connected(M hN, M hE, M hS, M hW, int w, i
 // (host table ea/eb/ed/erev); an edge pair stays removed iff start->end stays connected, which is
 // exactly the outcome of the reference's BFS-path test + re-add.  A removed edge whose two tiles
 // still share an intact 4-cycle cannot disconnect anything; otherwise still_connected decides.
-template <typename M>
+template <typename M, int NW>
 __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, int gl_t, M& hN, M& hE, M& hS, M& hW) {
   const int w = c.tw;
-  Bits256 L;
+  EdgeBits<NW> L;
   L.init(c.n_edges);
   int nrem = c.n_edges, count = c.n_edges;
   while (count > c.keep && nrem > 0) {
-    int k = (int)pcg_int(r, (uint32_t)nrem);
-    int e = L.select(k);
-    int e2 = sT.erev[e];
+    const int k = (int)pcg_draw(r, true, (uint32_t)nrem);  // nrem >= 2: always draws
+    const int e = L.select(k);
+    const uint32_t pk = sT.epk[e];
     L.clear(e);
-    L.clear(e2);
+    L.clear((int)(pk >> 24));
     nrem -= 2;
-    int a = sT.ea[e], b = sT.eb[e], d = sT.ed[e];
-    if (d == 0 || d == 3) {  // orient: a = north/west tile, d in {E (1), S (2)}
-      int t = a; a = b; b = t;
-      d = d == 0 ? 2 : 1;
-    }
+    const int a = (int)(pk & 255u), b = (int)((pk >> 8) & 255u), d = (int)((pk >> 16) & 255u);
     const M ma = (M)1 << a, mb = (M)1 << b;
     const M sN = hN, sE = hE, sS = hS, sW = hW;
     bool cyc;
     if (d == 1) {  // horizontal a | b
       hE &= ~ma;
       hW &= ~mb;
-      bool up = (hN & ma) && (hN & mb) && (hE & (ma >> w));
-      bool dn = (hS & ma) && (hS & mb) && (hE & (ma << w));
+      const bool up = (hN & ma) && (hN & mb) && (hE & (ma >> w));
+      const bool dn = (hS & ma) && (hS & mb) && (hE & (ma << w));
       cyc = up || dn;
     } else {       // vertical a over b
       hS &= ~ma;
       hN &= ~mb;
-      bool lf = (hW & ma) && (hW & mb) && (hS & (ma >> 1));
-      bool rt = (hE & ma) && (hE & mb) && (hS & (ma << 1));
+      const bool lf = (hW & ma) && (hW & mb) && (hS & (ma >> 1));
+      const bool rt = (hE & ma) && (hE & mb) && (hS & (ma << 1));
       cyc = lf || rt;
     }
     count -= 2;
@@ -326,6 +334,19 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, 
       hN = sN; hE = sE; hS = sS; hW = sW;
       count += 2;
     }
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ void add_border_connections(const DevCfg& c, Pcg& r, uint16_t* plan) {
+  EdgeBits<NW> B;
+  B.init(c.n_border);
+  int nb = c.n_border;
+  for (int k = 0; k < c.n_border_add; k++) {
+    const int j = B.select((int)pcg_int(r, (uint32_t)nb));
+    B.clear(j);
+    nb--;
+    plan[sT.bt[j]] |= (uint16_t)(1u << sT.bd[j]);
   }
 }
 
@@ -380,11 +401,12 @@ __device__ __forceinline__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* 
   STAMP(14);
   if (c.nt <= 32) {
     uint32_t n = (uint32_t)c.h0[0], e = (uint32_t)c.h0[1], so = (uint32_t)c.h0[2], we = (uint32_t)c.h0[3];
-    remove_edges<uint32_t>(c, r, st_t, gl_t, n, e, so, we);
+    if (c.n_edges <= 64) remove_edges<uint32_t, 1>(c, r, st_t, gl_t, n, e, so, we);
+    else remove_edges<uint32_t, 2>(c, r, st_t, gl_t, n, e, so, we);
     hN = n; hE = e; hS = so; hW = we;
   } else {
     hN = c.h0[0]; hE = c.h0[1]; hS = c.h0[2]; hW = c.h0[3];
-    remove_edges<uint64_t>(c, r, st_t, gl_t, hN, hE, hS, hW);
+    remove_edges<uint64_t, 4>(c, r, st_t, gl_t, hN, hE, hS, hW);
   }
   STAMP(15);
   // map_graph_to_tile_map_object (map_generator.py:269-334): exits straight into the LDS plan
@@ -394,15 +416,8 @@ __device__ __forceinline__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* 
   plan[st_t] |= (uint16_t)(1u << st_d);
   plan[gl_t] |= (uint16_t)(1u << gl_d);
   // add_connections_to_borders (map_generator.py:337-371), candidate list from the host
-  Bits256 B;
-  B.init(c.n_border);
-  int nb = c.n_border;
-  for (int k = 0; k < c.n_border_add; k++) {
-    int j = B.select((int)pcg_int(r, (uint32_t)nb));
-    B.clear(j);
-    nb--;
-    plan[sT.bt[j]] |= (uint16_t)(1u << sT.bd[j]);
-  }
+  if (c.n_border <= 64) add_border_connections<1>(c, r, plan);
+  else add_border_connections<3>(c, r, plan);
   // add_obstacles_to_map (map_generator.py:374-472)
   if (c.obstacle_probability > 0.0) {
     for (int t = 0; t < c.nt; t++) {
@@ -2050,10 +2065,14 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     memcpy(t.spawner, hs::kLaneSpawner, sizeof t.spawner);
     memcpy(t.lanes, hs::kLanes, sizeof t.lanes);
     memcpy(t.ind, c.ind_reward, sizeof t.ind);
-    memcpy(t.ea, c.ea, sizeof t.ea);
-    memcpy(t.eb, c.eb, sizeof t.eb);
-    memcpy(t.ed, c.ed, sizeof t.ed);
-    memcpy(t.erev, c.erev, sizeof t.erev);
+    for (int e = 0; e < c.n_edges; e++) {
+      int a = c.ea[e], b = c.eb[e], d = c.ed[e];
+      if (d == 0 || d == 3) {  // orient: a = north/west tile, d in {E (1), S (2)}
+        std::swap(a, b);
+        d = d == 0 ? 2 : 1;
+      }
+      t.epk[e] = (uint32_t)a | (uint32_t)b << 8 | (uint32_t)d << 16 | (uint32_t)c.erev[e] << 24;
+    }
     memcpy(t.bt, c.bt, sizeof t.bt);
     memcpy(t.bd, c.bd, sizeof t.bd);
     memset(t.li, 255, sizeof t.li);
@@ -2097,7 +2116,12 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     // the observation writes; large batches keep a full workgroup of env lanes for occupancy.
     // Traffic keeps 64 envs (one wave of car loops) per workgroup and sizes the observation
     // sub-batch so that two workgroups share a CU's 160 KiB of LDS when the counters allow it.
-    int envs = (n_envs <= (uint64_t)64 * 1024 || c.need_car) ? 64 : kBlock;
+    // Small batches: fewer envs per workgroup so that every CU gets one (a workgroup's time is the
+    // slowest of its lanes' serial chains); traffic: 64 (LDS).
+    int envs = c.need_car ? 64
+             : n_envs <= (uint64_t)8 * 1024 ? 16
+             : n_envs <= (uint64_t)16 * 1024 ? 32
+             : n_envs <= (uint64_t)64 * 1024 ? 64 : kBlock;
     if (const char* e = getenv("PGTG_ENVS_PER_BLOCK")) envs = atoi(e);
     if (envs != 16 && envs != 32 && envs != 64 && envs != 128 && envs != kBlock) envs = kBlock;
     while (envs > 16 && lds_bytes(lds_layout(c, envs)) + sizeof(Tables) > 150 * 1024) envs /= 2;

@@ -1,0 +1,44 @@
+"""FlattenObservation layout of the PGTG observation (pgtg/train.py:39-40) for batched tensors.
+
+gymnasium's `Dict` space orders a plain-dict's keys by name, and `flatten` concatenates its
+subspaces in that order: `MultiBinary((w, w))` as the w*w values row-major, `Discrete(n, start)` as a
+one-hot of length n at `x - start`, `MultiDiscrete(nvec)` as one one-hot per component, `Box` as its
+values.  For the PGTG space (environment.py:415-441) that is
+
+    map/<features sorted by name> (w*w each) | next_subgoal_direction (9, one-hot of d+1) |
+    position (9 + 9 one-hots) | velocity (2)
+
+`flatten_obs` builds that vector for every env of a batch directly from the device tensors of a
+`PGTGVecEnv` observation (no host round trip).
+"""
+from __future__ import annotations
+
+
+def flat_layout(spec) -> list[tuple[str, int]]:
+    """(field, width) in gymnasium's flatten order."""
+    win = spec.window
+    out = [(f"map/{k}", win * win) for k in sorted(k for k, _ in spec.channels)]
+    if spec.next_subgoal:
+        out.append(("next_subgoal_direction", 9))
+    out += [("position", 18), ("velocity", 2)]
+    return out
+
+
+def flat_dim(spec) -> int:
+    return sum(w for _, w in flat_layout(spec))
+
+
+def flatten_obs(spec, obs: dict, dtype=None):
+    """obs: a PGTGVecEnv observation dict ({"map": {k: [N, w, w]}, "position": [N, 2], ...}) ->
+    [N, flat_dim] tensor (float32 by default) on the same device."""
+    import torch
+    dtype = torch.float32 if dtype is None else dtype
+    pos = obs["position"].long()
+    n = pos.shape[0]
+    parts = [obs["map"][k].reshape(n, -1).to(dtype) for k in sorted(obs["map"])]
+    if spec.next_subgoal:
+        parts.append(torch.nn.functional.one_hot(obs["next_subgoal_direction"].long() + 1, 9).to(dtype))
+    parts.append(torch.nn.functional.one_hot(pos[:, 0].clamp(0, 8), 9).to(dtype))
+    parts.append(torch.nn.functional.one_hot(pos[:, 1].clamp(0, 8), 9).to(dtype))
+    parts.append(obs["velocity"].to(dtype))
+    return torch.cat(parts, dim=1)

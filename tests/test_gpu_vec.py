@@ -1,0 +1,102 @@
+"""Vector-env features beyond the golden replays: in-kernel TimeLimit truncation (pgtg/train.py:39)
+and the SB3 VecEnv adapter with FlattenObservation vectors (pgtg/train.py:40,54), against the
+CPU oracle driven the way the wrappers drive the reference."""
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+import helpers  # noqa: F401
+from oracle.oracle import OracleEnv
+from pgtg_amd import config as cfg
+from pgtg_amd.flat import flatten_obs
+
+pytestmark = pytest.mark.gpu
+
+
+def _spec(**kw):
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        return cfg.make_spec(**kw)
+
+
+def _oracle_obs_dict(spec, r):
+    keys = [k for k, _ in spec.channels]
+    o = {"map": {k: torch.as_tensor(r["obs"][c][None]) for c, k in enumerate(keys)},
+         "position": torch.as_tensor(np.array([r["pos"]], np.int32)),
+         "velocity": torch.as_tensor(np.array([r["vel"]], np.int32))}
+    if spec.next_subgoal:
+        o["next_subgoal_direction"] = torch.as_tensor(np.array([r["nsd"]], np.int32))
+    return o
+
+
+def test_time_limit_truncates_and_resets_in_kernel():
+    from pgtg_amd.vector import PGTGVecEnv
+    spec = _spec(random_map_width=3, random_map_height=3, use_next_subgoal_direction=True)
+    N, L = 12, 5
+    vec = PGTGVecEnv(N, spec=spec, autoreset=True, max_episode_steps=L)
+    vec.reset(seed=40)
+    orcs = [OracleEnv(spec) for _ in range(N)]
+    for i, o in enumerate(orcs):
+        o.reset(40 + i)
+    elapsed = np.zeros(N, int)
+    rng = np.random.default_rng(5)
+    truncs = 0
+    for t in range(3 * L):
+        acts = np.where(rng.random(N) < 0.8, 4, rng.integers(0, 9, N)).astype(np.uint8)  # mostly stand still
+        vec.step(torch.as_tensor(acts))
+        torch.cuda.synchronize()
+        term, trunc = vec.terminated.cpu().numpy(), vec.truncated.cpu().numpy()
+        m, fm = vec.obs_map.cpu().numpy(), vec.final_map.cpu().numpy()
+        for i in range(N):
+            r = orcs[i].step(int(acts[i]))
+            elapsed[i] += 1
+            want_trunc = elapsed[i] >= L  # TimeLimit: truncated when the step budget is used up
+            assert bool(term[i]) == r["terminated"], (t, i)
+            assert bool(trunc[i]) == want_trunc, (t, i)
+            if term[i] or trunc[i]:
+                assert np.array_equal(fm[i], r["obs"]), (t, i)
+                r = orcs[i].reset(None)
+                elapsed[i] = 0
+                truncs += int(trunc[i])
+            assert np.array_equal(m[i], r["obs"]), (t, i)
+    assert truncs > 0
+    vec.close()
+
+
+def test_sb3_adapter_flattened_obs_and_terminal_infos():
+    from pgtg_amd.sb3 import PGTGSB3VecEnv
+    kw = dict(random_map_width=3, random_map_height=3, use_next_subgoal_direction=True)
+    spec = _spec(**kw)
+    N, L = 8, 6
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        env = PGTGSB3VecEnv(N, max_episode_steps=L, seed=70, **kw)
+    obs = env.reset()
+    orcs = [OracleEnv(spec) for _ in range(N)]
+    rs = [o.reset(70 + i) for i, o in enumerate(orcs)]
+    for i in range(N):
+        assert np.array_equal(obs[i], flatten_obs(spec, _oracle_obs_dict(spec, rs[i])).numpy()[0])
+    elapsed = np.zeros(N, int)
+    rng = np.random.default_rng(9)
+    seen_done = 0
+    for t in range(20):
+        acts = rng.integers(0, 9, N)
+        obs, rew, dones, infos = env.step(acts)
+        for i in range(N):
+            r = orcs[i].step(int(acts[i]))
+            elapsed[i] += 1
+            assert np.float32(r["reward"]) == rew[i]
+            done = r["terminated"] or elapsed[i] >= L
+            assert bool(dones[i]) == done, (t, i)
+            if done:
+                term_flat = flatten_obs(spec, _oracle_obs_dict(spec, r)).numpy()[0]
+                assert np.array_equal(infos[i]["terminal_observation"], term_flat)
+                assert infos[i]["TimeLimit.truncated"] == (not r["terminated"])
+                r = orcs[i].reset(None)
+                elapsed[i] = 0
+                seen_done += 1
+            assert np.array_equal(obs[i], flatten_obs(spec, _oracle_obs_dict(spec, r)).numpy()[0]), (t, i)
+    assert seen_done > 0
+    env.close()
