@@ -193,10 +193,11 @@ uint64_t pgtg_num_envs(const pgtg_handle* h);
 /* Launch geometry of the step kernel: envs per 256-lane workgroup and dynamic LDS bytes. */
 int pgtg_launch_info(const pgtg_handle* h, int32_t* envs_per_block, int32_t* lds_bytes);
 const char* pgtg_last_error(const pgtg_handle* h);
-/* Per-launch device timing of the step kernel with HIP events on the handle's stream.  When enabled,
- * every pgtg_step brackets its kernel with an event pair; pgtg_timing_read synchronises and returns
- * the summed kernel milliseconds and the number of timed launches (reset=1 clears the tally). */
-int pgtg_enable_timing(pgtg_handle* h, int32_t on);
+/* Per-launch device timing of the step kernels with HIP events on the handle's stream.  every > 0:
+ * every every-th pgtg_step brackets its kernels with an event pair (1: all; 0: off);
+ * pgtg_timing_read synchronises and returns the summed milliseconds of the bracketed launches and
+ * their number (reset=1 clears the tally). */
+int pgtg_enable_timing(pgtg_handle* h, int32_t every);
 int pgtg_timing_read(pgtg_handle* h, double* total_ms, uint64_t* launches, int32_t reset);
 
 #ifdef __cplusplus

@@ -1311,6 +1311,7 @@ struct Lds {
   int seg_words;       // per-env observation words (n_channels * mask_words)
   int sub_envs;        // envs per observation sub-batch (== envs when they all fit)
   int stream_words;    // observation image words (+2 pad)
+  int spread;          // env slots spread over the four waves (traffic: long per-lane chains)
 };
 
 __host__ __device__ inline int odd_up(int x) { return x | 1; }
@@ -1327,6 +1328,7 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   int sub = l.seg_words > 0 ? (budget_words - 2) / l.seg_words : envs;
   l.sub_envs = sub > envs ? envs : (sub < 1 ? 1 : sub);
   l.stream_words = l.sub_envs * l.seg_words + 2;
+  l.spread = c.need_car ? 1 : 0;
   return l;
 }
 __host__ inline size_t lds_bytes(const Lds& l) {
@@ -1355,14 +1357,13 @@ template <bool TR>
 __device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
                                          const PgtgOutputs& o, uint8_t* dst, uint64_t env0, int nb, bool want,
                                          bool final, const uint8_t* sel, uint32_t* st, const Lds& L,
-                                         const uint8_t* occ) {
-  const int tid = threadIdx.x;
+                                         const uint8_t* occ, int slot) {
   for (int sb = 0; sb < nb; sb += L.sub_envs) {
     const int cnt = min(L.sub_envs, nb - sb);
-    if (want && tid >= sb && tid < sb + cnt) {
+    if (want && slot >= sb && slot < sb + cnt) {
       ObsInfo oi;
-      build_obs<TR>(c, S, pl, v, st + (tid - sb) * L.seg_words, oi, occ);
-      write_small_outputs(c, o, env0 + tid, v, oi, final);
+      build_obs<TR>(c, S, pl, v, st + (slot - sb) * L.seg_words, oi, occ);
+      write_small_outputs(c, o, env0 + slot, v, oi, final);
     }
     __syncthreads();
     if (dst)
@@ -1393,9 +1394,14 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   }
   const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
   const int nb = (int)min((uint64_t)L.envs, S.n - env0);
-  const uint64_t i = env0 + tid;
-  const bool live = tid < nb;
-  const int my_slot = tid < L.envs ? tid : 0;
+  // env slots: E/4 per wave when a workgroup holds fewer than 256 envs, so that all four SIMDs
+  // work and a wave's divergence spans fewer envs; contiguous envs per wave (coalesced rows)
+  const int per_wave = (!L.spread || L.envs >= kBlock) ? 64 : L.envs / 4;
+  const bool has_slot = (tid & 63) < per_wave;
+  const int slot = has_slot ? (tid >> 6) * per_wave + (tid & 63) : 0;
+  const uint64_t i = env0 + slot;
+  const bool live = has_slot && slot < nb;
+  const int my_slot = slot;
   uint32_t* plan_w = lds + my_slot * L.plan_stride_dw;
   uint32_t* scr_w = lds + L.envs * L.plan_stride_dw + my_slot * L.scratch_dw;
   uint32_t* traf_w = lds + L.envs * (L.plan_stride_dw + L.scratch_dw) + my_slot * L.traf_dw;
@@ -1479,7 +1485,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       my_sel = do_reset ? 2 : 0;
     }
   }
-  sel[tid] = my_sel;
+  if (has_slot) sel[slot] = my_sel;
   STAMP(2);
   const bool single = L.sub_envs >= nb;  // the whole workgroup's image fits: build once, rebuild resets
   const int n_final = __syncthreads_count(my_sel == 1);
@@ -1487,7 +1493,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (single) {
     if (live && (my_sel != 2)) {
       ObsInfo oi;
-      build_obs<TR>(c, S, pl, v, st + tid * L.seg_words, oi, occ);
+      build_obs<TR>(c, S, pl, v, st + slot * L.seg_words, oi, occ);
       write_small_outputs(c, out, i, v, oi, my_sel == 1);
     }
     __syncthreads();
@@ -1495,7 +1501,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
                 (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel);
   } else if (want_final) {
-    obs_pass<TR>(c, S, pl, v, out, out.final_obs, env0, nb, my_sel == 1, true, sel, st, L, occ);
+    obs_pass<TR>(c, S, pl, v, out, out.final_obs, env0, nb, my_sel == 1, true, sel, st, L, occ, slot);
   }
   STAMP(3);
   const bool reset_now = my_sel != 0;
@@ -1537,7 +1543,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (single) {
     if (reset_now) {
       ObsInfo oi;
-      build_obs<TR>(c, S, pl, v, st + tid * L.seg_words, oi, nullptr);  // cars come from k_traffic
+      build_obs<TR>(c, S, pl, v, st + slot * L.seg_words, oi, nullptr);  // cars come from k_traffic
       write_small_outputs(c, out, i, v, oi, false);
     }
     __syncthreads();
@@ -1545,7 +1551,8 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
                 (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, nullptr);
   } else {
-    obs_pass<TR>(c, S, pl, v, out, out.obs, env0, nb, live, false, nullptr, st, L, reset_now ? nullptr : occ);
+    obs_pass<TR>(c, S, pl, v, out, out.obs, env0, nb, live, false, nullptr, st, L, reset_now ? nullptr : occ,
+                 slot);
   }
   if (mode == MODE_STEP && tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
   STAMP(6);
@@ -1553,26 +1560,31 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
 
 // Initial traffic of the envs k_env reset in this launch (its work list), one lane per env with
 // the reset scratch in LDS; the observation k_env wrote for them gets the new cars' squares.
-__global__ void __launch_bounds__(64) k_traffic(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
-                                                DevState S, PgtgOutputs out, uint32_t tr_slot, int plan_dw, int rs_dw) {
+// `lanes` envs per 256-lane workgroup, lanes/4 per wave (all four SIMDs, narrower divergence).
+__global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
+                                                    DevState S, PgtgOutputs out, uint32_t tr_slot, int plan_dw,
+                                                    int rs_dw, int lanes) {
   extern __shared__ uint32_t lds[];
   const DevCfg& c = *cfg;
   const uint32_t n = S.tr_count[tr_slot];
-  const uint32_t j0 = blockIdx.x * blockDim.x;
+  const uint32_t j0 = blockIdx.x * (uint32_t)lanes;
   if (j0 >= n) return;  // whole workgroup idle
-  const int tid = threadIdx.x;
+  const int per_wave = lanes / 4;
+  const int tid0 = threadIdx.x;
+  const bool has_slot = (tid0 & 63) < per_wave;
+  const int tid = has_slot ? (tid0 >> 6) * per_wave + (tid0 & 63) : 0;
   {
     const int words = (int)(sizeof(Tables) / 4);
     const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
     uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
-    for (int k = tid; k < words; k += blockDim.x) dstt[k] = src[k];
+    for (int k = tid0; k < words; k += blockDim.x) dstt[k] = src[k];
   }
   __syncthreads();
   const uint32_t j = j0 + tid;
-  if (j >= n) return;
+  if (!has_slot || j >= n) return;
   const uint64_t i = S.tr_list[j];
   uint32_t* plan_w = lds + tid * plan_dw;
-  uint8_t* rs = reinterpret_cast<uint8_t*>(lds + blockDim.x * plan_dw + tid * rs_dw);
+  uint8_t* rs = reinterpret_cast<uint8_t*>(lds + lanes * plan_dw + tid * rs_dw);
   const uint4* src = reinterpret_cast<const uint4*>(S.plan + i * (uint64_t)c.plan_stride);
   for (int k = 0; k < c.plan_stride / 8; k++) {
     uint4 w4 = src[k];
@@ -1678,7 +1690,8 @@ struct pgtg_handle {
   std::vector<void*> allocs;
   std::string err;
   uint64_t seed_offset = 0;  // global index of env 0 (for sharded runs)
-  bool timing = false;
+  int timing = 0;             // bracket every `timing`-th step launch with an event pair (0: off)
+  uint64_t step_launches = 0;
   std::vector<hipEvent_t> evpool;  // pairs (start, stop) per timed launch
   size_t ev_used = 0;
   double acc_ms = 0.0;
@@ -2135,7 +2148,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
       h->kt_plan_dw = odd_up((c.nt + 1) / 2);
       h->kt_rs_dw = odd_up(c.rs_bytes / 4);
       h->kt_lanes = 64;
-      while (h->kt_lanes > 8 && (size_t)4 * h->kt_lanes * (h->kt_plan_dw + h->kt_rs_dw) + sizeof(Tables) > 150 * 1024)
+      while (h->kt_lanes > 4 && (size_t)4 * h->kt_lanes * (h->kt_plan_dw + h->kt_rs_dw) + sizeof(Tables) > 150 * 1024)
         h->kt_lanes /= 2;
       h->kt_lds = (size_t)4 * h->kt_lanes * (h->kt_plan_dw + h->kt_rs_dw);
       if (h->kt_lds + sizeof(Tables) > 160 * 1024) {
@@ -2185,7 +2198,7 @@ int pgtg_set_outputs(pgtg_handle* h, const PgtgOutputs* o) {
 static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, int mode) {
   HIPCHK(h, hipSetDevice(h->device));
   uint64_t blocks = (h->n + h->L.envs - 1) / h->L.envs;
-  const bool timed = h->timing && mode == MODE_STEP;
+  const bool timed = h->timing > 0 && mode == MODE_STEP && (h->step_launches++ % (uint64_t)h->timing) == 0;
   if (timed) {
     if (h->evpool.empty()) {
       h->evpool.resize(2048);
@@ -2208,8 +2221,8 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
     // initial traffic of the envs reset by this launch, then (windows other than the agent's tile)
     // their observation again with the cars
     const uint64_t kb = (h->n + h->kt_lanes - 1) / h->kt_lanes;
-    hipLaunchKernelGGL(k_traffic, dim3((unsigned)kb), dim3(h->kt_lanes), h->kt_lds, h->stream, h->dcfg, h->dtab, h->S,
-                       h->out, h->tr_slot, h->kt_plan_dw, h->kt_rs_dw);
+    hipLaunchKernelGGL(k_traffic, dim3((unsigned)kb), dim3(kBlock), h->kt_lds, h->stream, h->dcfg, h->dtab, h->S,
+                       h->out, h->tr_slot, h->kt_plan_dw, h->kt_rs_dw, h->kt_lanes);
     HIPCHK(h, hipGetLastError());
     if (!h->hcfg.obs_fast && h->hcfg.traffic_ch >= 0) {
       PgtgOutputs o{};
@@ -2479,7 +2492,8 @@ const char* pgtg_last_error(const pgtg_handle* h) { return h ? h->err.c_str() : 
 
 int pgtg_enable_timing(pgtg_handle* h, int32_t on) {
   if (!h) return PGTG_E_INVALID;
-  h->timing = on != 0;
+  h->timing = on < 0 ? 0 : on;
+  h->step_launches = 0;
   return PGTG_OK;
 }
 

@@ -172,6 +172,22 @@ class PGTGVecEnv:
                                              C.c_uint64(t)), self._h)
         _check(self._lib.pgtg_step(self._h, C.c_void_p(self.actions.data_ptr())), self._h)
 
+    def random_actions(self, steps: int, seed: int, t0: int = 0):
+        """[steps, N] uint8 device tensor of synthetic uniform actions (the same hash as step_random),
+        generated ahead so that a timed rollout starts with its inputs resident in HBM."""
+        import torch
+        self._bind_stream()
+        a = torch.empty((steps, self.num_envs), dtype=torch.uint8, device=self.device)
+        for k in range(steps):
+            _check(self._lib.pgtg_random_actions(self._h, C.c_void_p(a[k].data_ptr()), C.c_uint64(seed),
+                                                 C.c_uint64(t0 + k)), self._h)
+        return a
+
+    def step_actions(self, actions_row):
+        """One tick from a resident [N] uint8 device tensor, no host conversion or returned views."""
+        self._bind_stream()
+        _check(self._lib.pgtg_step(self._h, C.c_void_p(actions_row.data_ptr())), self._h)
+
     def observe(self):
         """Re-emit every env's observation (after set_agent / add_car)."""
         self._bind_stream()
@@ -267,8 +283,9 @@ class PGTGVecEnv:
         _check(self._lib.pgtg_get_counters(self._h, C.byref(a), C.byref(b)), self._h)
         return a.value, b.value
 
-    def enable_timing(self, on: bool = True):
-        self._lib.pgtg_enable_timing(self._h, int(on))
+    def enable_timing(self, every: int = 1):
+        """Bracket every `every`-th step launch with a HIP event pair (0: off)."""
+        self._lib.pgtg_enable_timing(self._h, int(every))
 
     def timing_read(self, reset: bool = True) -> tuple[float, int]:
         """(summed step-kernel ms, timed launches) from HIP events on the handle's stream."""
