@@ -178,7 +178,8 @@ int pgtg_get_map_plan(pgtg_handle* h, uint64_t env, int32_t* w, int32_t* h_, uin
 #define PGTG_SQ_TRAFFIC_LIGHT (1ull << 45)
 int pgtg_get_squares(pgtg_handle* h, uint64_t env, uint64_t* words, int32_t cap, int32_t* width, int32_t* height);
 int pgtg_set_agent(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t vx, int32_t vy);
-int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t route, int32_t profile);
+/* Append a car (env.cars.append(Car(...)) in the reference tests); car_id < 0 takes the env's next id. */
+int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t route, int32_t profile, int32_t car_id);
 /* Replace the traffic rules of every env (add_traffic_rule / remove_traffic_rule,
  * environment.py:569-575); takes effect from the next step.  n_rules <= PGTG_MAX_RULES. */
 int pgtg_set_rules(pgtg_handle* h, const PgtgRule* rules, int32_t n_rules);

@@ -88,7 +88,7 @@ def lib():
         L.orc_get_map_plan.argtypes = [C.c_void_p] + [C.c_void_p] * 7
         L.orc_get_misc.argtypes = [C.c_void_p] + [C.c_void_p] * 4
         L.orc_set_agent.argtypes = [C.c_void_p] + [C.c_int32] * 4
-        L.orc_add_car.argtypes = [C.c_void_p] + [C.c_int32] * 4
+        L.orc_add_car.argtypes = [C.c_void_p] + [C.c_int32] * 5
         L.orc_get_squares.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         L.orc_last_error.restype = C.c_char_p
         L.orc_last_error.argtypes = [C.c_void_p]
@@ -243,8 +243,8 @@ class OracleEnv:
         self._L.orc_set_agent(self._h, int(x), int(y), int(o.vel[0] if vx is None else vx),
                               int(o.vel[1] if vy is None else vy))
 
-    def add_car(self, x, y, route: int, profile: int):
-        self._L.orc_add_car(self._h, int(x), int(y), int(route), int(profile))
+    def add_car(self, x, y, route: int, profile: int, car_id: int = -1):
+        self._L.orc_add_car(self._h, int(x), int(y), int(route), int(profile), int(car_id))
 
     def squares(self) -> np.ndarray:
         n = self._L.orc_get_squares(self._h, None, 0)

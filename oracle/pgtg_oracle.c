@@ -1353,8 +1353,10 @@ int orc_set_agent(orc_env* e, int32_t x, int32_t y, int32_t vx, int32_t vy) {
   e->vy = vy;
   return 0;
 }
-int orc_add_car(orc_env* e, int32_t x, int32_t y, int32_t route, int32_t profile) {
-  push_car(e, (car_t){e->next_car_id++, x, y, route, profile, 0, 0});
+/* env.cars.append(Car(id, Position(x, y), route, profile)) of the reference tests; id < 0 takes the
+ * next id like _spawn_new_car (environment.py:970-1002), an explicit id leaves _next_car_id alone */
+int orc_add_car(orc_env* e, int32_t x, int32_t y, int32_t route, int32_t profile, int32_t id) {
+  push_car(e, (car_t){id < 0 ? e->next_car_id++ : id, x, y, route, profile, 0, 0});
   return 0;
 }
 int orc_get_squares(const orc_env* e, uint64_t* out, int cap) {

@@ -114,7 +114,7 @@ def lib():
         "pgtg_get_squares": ([vp, u64, vp, i32, C.POINTER(i32), C.POINTER(i32)], C.c_int),
         "pgtg_set_rules": ([vp, vp, i32], C.c_int),
         "pgtg_set_agent": ([vp, u64, i32, i32, i32, i32], C.c_int),
-        "pgtg_add_car": ([vp, u64, i32, i32, i32, i32], C.c_int),
+        "pgtg_add_car": ([vp, u64, i32, i32, i32, i32, i32], C.c_int),
         "pgtg_observe": ([vp], C.c_int),
         "pgtg_get_counters": ([vp, C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "pgtg_error_count": ([vp, C.POINTER(u64), C.POINTER(i32)], C.c_int),

@@ -2423,7 +2423,7 @@ int pgtg_set_agent(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t v
   return PGTG_OK;
 }
 
-int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t route, int32_t profile) {
+int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t route, int32_t profile, int32_t car_id) {
   if (!h || env >= h->n) return PGTG_E_INVALID;
   if (!h->hcfg.need_car) return fail(h, PGTG_E_UNSUPPORTED, "create the handle with min_car_capacity > 0 or traffic");
   if (x < 0 || y < 0 || x >= h->hcfg.W || y >= h->hcfg.H || route < 0 || route >= 20 || profile < 0 || profile >= 5)
@@ -2435,12 +2435,13 @@ int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t rou
   int nc = (int)(t.x & 0xffffu), bank = (int)t.z;
   if (nc >= h->hcfg.car_cap) return fail(h, PGTG_E_UNSUPPORTED, "car capacity exhausted");
   const uint64_t a = ((uint64_t)bank * h->hcfg.car_cap + nc) * h->n + env;
-  uint32_t w0 = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)profile << 21, w1 = 0, id = t.y;
+  uint32_t w0 = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)profile << 21, w1 = 0;
+  const uint32_t id = car_id < 0 ? t.y : (uint32_t)car_id;
   HIPCHK(h, hipMemcpy(h->S.car_w0 + a, &w0, 4, hipMemcpyHostToDevice));
   HIPCHK(h, hipMemcpy(h->S.car_w1 + a, &w1, 4, hipMemcpyHostToDevice));
   HIPCHK(h, hipMemcpy(h->S.car_id + a, &id, 4, hipMemcpyHostToDevice));
   t.x = (t.x & 0xffff0000u) | (uint32_t)(nc + 1);
-  t.y += 1;
+  if (car_id < 0) t.y += 1;
   HIPCHK(h, hipMemcpy(h->S.traf + env, &t, sizeof t, hipMemcpyHostToDevice));
   return PGTG_OK;
 }

@@ -18,12 +18,82 @@ effect") like the reference (:1109-1110).  Differences, by design:
 from __future__ import annotations
 
 import math
-from typing import Any
+from dataclasses import dataclass
+from enum import Enum
+from typing import Any, NamedTuple
 
 import numpy as np
 
 from . import config as _cfg
 from .vector import PGTGVecEnv
+
+
+class Position(NamedTuple):  # environment.py:33-35
+    x: int
+    y: int
+
+
+class DriverProfile(Enum):  # environment.py:38-45
+    CONSERVATIVE = "conservative"
+    NORMAL = "normal"
+    AGGRESSIVE = "aggressive"
+    ELDERLY = "elderly"
+    RECKLESS = "reckless"
+
+
+@dataclass
+class Car:  # environment.py:112-120 (a snapshot; appending one to env.cars adds it on the device)
+    id: int
+    position: Position
+    route: str
+    driver_profile: DriverProfile = DriverProfile.NORMAL
+    patience_counter: int = 0
+    last_action_delay: int = 0
+    stuck_counter: int = 0
+
+
+class CarList(list):
+    """`env.cars`: the device car list as Car snapshots; `append` adds a car to the episode."""
+
+    def __init__(self, env: "PGTGEnv", cars):
+        super().__init__(cars)
+        self._env = env
+
+    def append(self, car: Car) -> None:  # noqa: D401
+        prof = car.driver_profile.value if isinstance(car.driver_profile, DriverProfile) else str(car.driver_profile)
+        self._env._vec.add_car(0, int(car.position[0]), int(car.position[1]), _cfg.ROUTES.index(car.route),
+                               _cfg.DRIVER_PROFILES.index(prof), int(car.id))
+        self._env._vec.observe()
+        super().append(car)
+
+
+_SQ_NAMES = {"wall": 1 << 32, "car_spawner": 1 << 37, "start": 1 << 38, "subgoal": 1 << 39,
+             "used subgoal": 1 << 40, "final goal": 1 << 41, "ice": 1 << 42, "broken road": 1 << 43,
+             "sand": 1 << 44, "traffic_light": 1 << 45}
+
+
+class EpisodeMapView:
+    """Read-only `env.map` (pgtg/map.py:8-184) over the device map's square feature words."""
+
+    def __init__(self, words: np.ndarray):
+        self._w = words
+        self.width, self.height = words.shape
+
+    def inside_map(self, x: int, y: int) -> bool:
+        return 0 <= x < self.width and 0 <= y < self.height
+
+    def get_features_at(self, x: int, y: int) -> set[str]:
+        if not self.inside_map(x, y):
+            raise ValueError("coordinates are outside the map")
+        w = int(self._w[x, y])
+        out = {n for n, b in _SQ_NAMES.items() if w & b}
+        out |= {_cfg.LANES[k] for k in range(32) if (w >> k) & 1}
+        return out
+
+    def feature_at(self, x: int, y: int, features) -> bool:
+        names = [features] if isinstance(features, str) else list(features)
+        return not self.get_features_at(x, y).isdisjoint(names)
+
 
 _AGENT_DIR_NAMES = ["south_to_north", "south_to_north", "west_to_east", "west_to_east",
                     "north_to_south", "north_to_south", "east_to_west", "east_to_west"]
@@ -90,7 +160,8 @@ class PGTGEnv:
         self.render_mode = None
         self.spec = _cfg.make_spec(map_path, **kwargs)
         self.map_path = map_path
-        self._vec = PGTGVecEnv(1, spec=self.spec, device=device, autoreset=False)
+        # room for cars appended by hand (env.cars.append(Car(...)), as the reference tests do)
+        self._vec = PGTGVecEnv(1, spec=self.spec, device=device, autoreset=False, min_car_capacity=64)
         self.action_space, self.observation_space = _spaces(self.spec)
         self.features_to_include_in_observation = [k for k, _ in self.spec.channels]
         self.terminated = False
@@ -171,15 +242,23 @@ class PGTGEnv:
         return bool(self._vec.env_state(0)["flat_tire"])
 
     @property
-    def cars(self) -> list[dict[str, Any]]:
-        return [{"id": int(c[0]), "x": int(c[1]), "y": int(c[2]), "route": _cfg.ROUTES[int(c[3])],
-                 "driver_profile": _cfg.DRIVER_PROFILES[int(c[4])], "patience_counter": int(c[5])}
-                for c in self._vec.cars(0)]
+    def cars(self) -> CarList:
+        return CarList(self, [Car(int(c[0]), Position(int(c[1]), int(c[2])), _cfg.ROUTES[int(c[3])],
+                                  DriverProfile(_cfg.DRIVER_PROFILES[int(c[4])]), int(c[5]), int(c[6]))
+                              for c in self._vec.cars(0)])
 
-    def add_car(self, x: int, y: int, route: str, driver_profile: str = "normal") -> None:
-        """Append a car like `env.cars.append(Car(...))` in the reference tests."""
-        self._vec.add_car(0, x, y, _cfg.ROUTES.index(route), _cfg.DRIVER_PROFILES.index(driver_profile))
-        self._vec.observe()
+    def _info_cars(self) -> list[dict[str, Any]]:
+        return [{"id": c.id, "x": c.position.x, "y": c.position.y, "route": c.route,
+                 "driver_profile": c.driver_profile.value, "patience_counter": c.patience_counter}
+                for c in self.cars]
+
+    @property
+    def map(self) -> EpisodeMapView:
+        return EpisodeMapView(self._vec.squares(0))
+
+    @property
+    def _next_car_id(self) -> int:
+        return int(self._vec.env_state(0)["next_car_id"])
 
     def map_plan(self) -> dict:
         return self._vec.map_plan(0)
@@ -206,7 +285,7 @@ class PGTGEnv:
 
     # -- info (environment.py:1538-1578) --------------------------------------------------------
     def get_driver_profile_stats(self, cars: list[dict] | None = None) -> dict:
-        cars = self.cars if cars is None else cars
+        cars = self._info_cars() if cars is None else cars
         counts = {p: 0 for p in _cfg.DRIVER_PROFILES}
         for c in cars:
             counts[c["driver_profile"]] += 1
@@ -223,7 +302,7 @@ class PGTGEnv:
         tx = max(0, min(int(st["x"] // 9), plan["w"] - 1))
         ty = max(0, min(int(st["y"] // 9), plan["h"] - 1))
         ex = plan["exits"][ty * plan["w"] + tx]
-        cars = self.cars if self.spec.traffic_density > 0 or st["n_cars"] else []
+        cars = self._info_cars() if st["n_cars"] else []
         names = self._vec.rule_names()
         return {
             "x": st["x"], "y": st["y"], "x_velocity": st["vx"], "y_velocity": st["vy"],

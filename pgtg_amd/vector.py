@@ -38,7 +38,7 @@ def _check(rc: int, handle=None) -> None:
 class PGTGVecEnv:
     def __init__(self, num_envs: int, map_path: str | None = None, *, device: int | None = None,
                  autoreset: bool = True, max_episode_steps: int | None = None, spec: EnvSpec | None = None,
-                 **kwargs: Any):
+                 min_car_capacity: int = 0, **kwargs: Any):
         import torch
 
         self.spec = spec if spec is not None else make_spec(map_path, **kwargs)
@@ -49,7 +49,7 @@ class PGTGVecEnv:
             device = torch.cuda.current_device()
         self.device = torch.device("cuda", device)
         self._lib = _abi.lib()
-        self._cfg = _abi.config_struct(self.spec, autoreset, max_episode_steps)
+        self._cfg = _abi.config_struct(self.spec, autoreset, max_episode_steps, min_car_capacity)
         h = C.c_void_p()
         _check(self._lib.pgtg_create(C.byref(self._cfg), self.num_envs, int(device), C.byref(h)), None)
         self._h = h
@@ -264,8 +264,9 @@ class PGTGVecEnv:
     def set_agent(self, i: int, x: int, y: int, vx: int, vy: int):
         _check(self._lib.pgtg_set_agent(self._h, i, x, y, vx, vy), self._h)
 
-    def add_car(self, i: int, x: int, y: int, route: int, profile: int):
-        _check(self._lib.pgtg_add_car(self._h, i, x, y, route, profile), self._h)
+    def add_car(self, i: int, x: int, y: int, route: int, profile: int, car_id: int = -1):
+        """Append a car to env i (car_id < 0: the env's next id)."""
+        _check(self._lib.pgtg_add_car(self._h, i, x, y, route, profile, car_id), self._h)
 
     def mean_cars(self, sample: int = 64) -> float:
         """Average car count over (up to) `sample` envs (host-synchronising)."""
