@@ -104,14 +104,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for a one-GPU box (never set by the driver): every rank on GPU 0, gloo counters
+    backend = os.environ.get("PGTG_BENCH_BACKEND", "nccl")  # nccl == RCCL over xGMI on MI355X
+    if os.environ.get("PGTG_BENCH_SAME_GPU") == "1":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     dev = torch.device("cuda", local)
+    red_dev = dev if backend == "nccl" else None
 
     from pgtg_amd.build import build
-    if rank == 0 and world == 1:
-        build()
+    build()  # no-op when the in-tree library is current (file-locked across ranks)
     from pgtg_amd.config import make_spec
     from pgtg_amd.dist import Shard, reduce_counters
     from pgtg_amd.vector import PGTGVecEnv
@@ -146,7 +150,7 @@ def main():
     kern_ms, launches = env.timing_read(reset=True)
     steps1, eps1 = env.counters()
     # RCCL (nccl backend) all-reduce: global env-step / episode counters (sum), slowest rank's time (max)
-    total_steps, total_eps, t_max = reduce_counters(steps1 - steps0, eps1 - eps0, elapsed, device=dev)
+    total_steps, total_eps, t_max = reduce_counters(steps1 - steps0, eps1 - eps0, elapsed, device=red_dev)
     value = total_steps / t_max
 
     if rank == 0:

@@ -23,11 +23,21 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    if force or needs_build():
-        cmd = [HIPCC, *FLAGS, "-o", OUT, SRC]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+    """(Re)build the library if a source is newer.  Serialised by a file lock so that the ranks of a
+    multi-process run can all call it: one compiles, the others wait and find it up to date."""
+    import fcntl
+    with open(OUT + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if force or needs_build():
+                tmp = OUT + f".tmp{os.getpid()}"
+                cmd = [HIPCC, *FLAGS, "-o", tmp, SRC]
+                if verbose:
+                    print(" ".join(cmd), flush=True)
+                subprocess.run(cmd, check=True)
+                os.replace(tmp, OUT)  # atomic: a concurrent loader never sees a partial file
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
     return OUT
 
 

@@ -100,3 +100,31 @@ def test_sb3_adapter_flattened_obs_and_terminal_infos():
             assert np.array_equal(obs[i], flatten_obs(spec, _oracle_obs_dict(spec, r)).numpy()[0]), (t, i)
     assert seen_done > 0
     env.close()
+
+
+def test_sharded_batch_equals_the_global_batch():
+    """bench/dist sharding: rank r's envs are seeded with r*n_local + i, so two half batches step
+    exactly like the global batch (pgtg_amd/dist.py)."""
+    from pgtg_amd.dist import Shard
+    from pgtg_amd.vector import PGTGVecEnv
+    spec = _spec(random_map_width=3, random_map_height=3, traffic_density=0.2)
+    n = 32
+    full = PGTGVecEnv(2 * n, spec=spec)
+    full.reset(seed=0)
+    halves = []
+    for r in range(2):
+        h = PGTGVecEnv(n, spec=spec)
+        h.reset(seed=Shard(r, 2, n).offset)
+        halves.append(h)
+    rng = np.random.default_rng(2)
+    for t in range(25):
+        a = torch.as_tensor(rng.integers(0, 9, 2 * n).astype(np.uint8))
+        full.step(a)
+        for r, h in enumerate(halves):
+            h.step(a[r * n:(r + 1) * n])
+        torch.cuda.synchronize()
+        for r, h in enumerate(halves):
+            assert torch.equal(full.obs_map[r * n:(r + 1) * n], h.obs_map), (t, r)
+            assert torch.equal(full.reward[r * n:(r + 1) * n], h.reward), (t, r)
+    for i in (0, n - 1, n, 2 * n - 1):
+        assert np.array_equal(full.cars(i), halves[i // n].cars(i % n))
