@@ -19,6 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <array>
 #include <cstddef>
 #include <string>
@@ -2139,6 +2140,24 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     if (envs != 16 && envs != 32 && envs != 64 && envs != 128 && envs != kBlock) envs = kBlock;
     while (envs > 16 && lds_bytes(lds_layout(c, envs)) + sizeof(Tables) > 150 * 1024) envs /= 2;
     h->L = lds_layout(c, envs);
+    if (!c.need_car && h->L.envs == kBlock) {
+      // Large batches: when the grid needs more workgroups per CU than fit the LDS (up to the 4 that
+      // the registers allow), observe in sub-batches so that the whole grid runs in one round.
+      const uint64_t blocks = (n_envs + kBlock - 1) / kBlock;
+      const int want = (int)std::min<uint64_t>(4, (blocks + 255) / 256);
+      auto fit = [&](const Lds& l) { return (int)((160 * 1024) / (lds_bytes(l) + sizeof(Tables))); };
+      while (fit(h->L) < want && h->L.sub_envs > 64) {
+        h->L.sub_envs /= 2;
+        h->L.stream_words = h->L.sub_envs * h->L.seg_words + 2;
+      }
+    }
+    if (const char* e = getenv("PGTG_OBS_SUB")) {  // tuning knob: observation sub-batch size
+      int sub = atoi(e);
+      if (sub >= 1 && sub < h->L.sub_envs) {
+        h->L.sub_envs = sub;
+        h->L.stream_words = sub * h->L.seg_words + 2;
+      }
+    }
     if (c.need_car) {
       while (h->L.sub_envs > 8 && lds_bytes(h->L) + sizeof(Tables) > 80 * 1024) {
         h->L.sub_envs /= 2;
