@@ -2135,7 +2135,8 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     int envs = c.need_car ? 64
              : n_envs <= (uint64_t)8 * 1024 ? 16
              : n_envs <= (uint64_t)16 * 1024 ? 32
-             : n_envs <= (uint64_t)64 * 1024 ? 64 : kBlock;
+             : n_envs <= (uint64_t)64 * 1024 ? 64
+             : n_envs <= (uint64_t)128 * 1024 ? 128 : kBlock;
     if (const char* e = getenv("PGTG_ENVS_PER_BLOCK")) envs = atoi(e);
     if (envs != 16 && envs != 32 && envs != 64 && envs != 128 && envs != kBlock) envs = kBlock;
     while (envs > 16 && lds_bytes(lds_layout(c, envs)) + sizeof(Tables) > 150 * 1024) envs /= 2;

@@ -40,7 +40,9 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
     _abi.lib().pgtg_read_stamps.argtypes = [C.c_void_p, C.c_uint64]
     _abi.lib().pgtg_read_stamps(buf.ctypes.data, buf.size)
     st = buf.reshape(nw, SLOTS).astype(np.int64)
-    active = np.ones(nw, bool)  # env slots are spread over all four waves
+    # traffic workgroups spread their env slots over all four waves; otherwise envs fill waves in order
+    spread = kw.get("traffic_density", 0) > 0
+    active = np.ones(nw, bool) if spread else (np.arange(nw) % 4) * 64 < E
     st = st[active]
     d = np.diff(st[:, :7], axis=1)
     print(f"{name}: {N} envs, {E} envs/workgroup, LDS {lds} B; cycles per active wave (last launch)", flush=True)
