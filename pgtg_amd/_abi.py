@@ -11,7 +11,8 @@ import os
 from . import config as cfgmod
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libpgtg_hip.so")
+# PGTG_LIB selects another build of the same library (test variants, pgtg_amd/build.py VARIANTS)
+LIB_PATH = os.environ.get("PGTG_LIB") or os.path.join(PKG, "libpgtg_hip.so")
 
 PGTG_ABI_VERSION = 1
 MAX_TILES = 64

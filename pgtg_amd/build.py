@@ -15,32 +15,45 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp
          "-Wall", "-Wno-unused-function"]
 
 
-def needs_build() -> bool:
-    if not os.path.exists(OUT):
+# test variant: occupancy counters saturating at 2 cars so that the exact-recount path runs often
+# (tests/test_gpu_occupancy.py replays the traffic trajectories through it)
+VARIANTS = {"occsat": ["-DPGTG_OCC_MAX=2"]}
+
+
+def variant_path(name: str) -> str:
+    return os.path.join(PKG, f"libpgtg_hip_{name}.so")
+
+
+def needs_build(out: str = OUT) -> bool:
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
+    t = os.path.getmtime(out)
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, variant: str | None = None) -> str:
     """(Re)build the library if a source is newer.  Serialised by a file lock so that the ranks of a
     multi-process run can all call it: one compiles, the others wait and find it up to date."""
     import fcntl
-    with open(OUT + ".lock", "w") as lk:
+    out = OUT if variant is None else variant_path(variant)
+    extra = [] if variant is None else VARIANTS[variant]
+    with open(out + ".lock", "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
         try:
-            if force or needs_build():
-                tmp = OUT + f".tmp{os.getpid()}"
-                cmd = [HIPCC, *FLAGS, "-o", tmp, SRC]
+            if force or needs_build(out):
+                tmp = out + f".tmp{os.getpid()}"
+                cmd = [HIPCC, *FLAGS, *extra, "-o", tmp, SRC]
                 if verbose:
                     print(" ".join(cmd), flush=True)
                 subprocess.run(cmd, check=True)
-                os.replace(tmp, OUT)  # atomic: a concurrent loader never sees a partial file
+                os.replace(tmp, out)  # atomic: a concurrent loader never sees a partial file
         finally:
             fcntl.flock(lk, fcntl.LOCK_UN)
-    return OUT
+    return out
 
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
+    for v in VARIANTS:
+        build(force="--force" in sys.argv, verbose=True, variant=v)
     print(OUT)

@@ -16,7 +16,7 @@ constexpr int kMaxBorder = 192;   // border-connection candidates (<= 2w+2h-2)
 constexpr int kMaxWin = PGTG_MAX_WINDOW;
 constexpr int kMaskWords = (kMaxWin * kMaxWin + 31) / 32;  // 8
 constexpr int kBlock = 256;       // lanes (= envs) per workgroup for the step kernels
-constexpr int kSpCache = 32;      // spawner-list entries k_env keeps in LDS (the rest are read from HBM)
+constexpr int kSpCache = 24;      // spawner-list entries k_env keeps in LDS (the rest are read from HBM)
 
 // agent flags (EnvRec.w2 bits 16..23)
 constexpr uint32_t kFlagTerminated = 1u << 0;

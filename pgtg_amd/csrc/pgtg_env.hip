@@ -179,15 +179,28 @@ __device__ __forceinline__ bool square_tlight(const DevCfg& c, const Plan& pl, i
   int sq = lx * 9 + ly;
   return plan_otype(p) == 4 && !bit81(sT.wall[plan_exits(p)], sq) && bit81(sT.obst[plan_omask(p)], sq);
 }
+// Occupancy counters are 4-bit (two lane slots per byte, 16 B per tile) so that 256 envs' counters
+// fit a CU's LDS.  A counter saturates at kOccMax and raises the lane's `sat` flag; decrementing a
+// saturated counter then recounts that square exactly from the car banks (rare: squares with 15
+// cars), so every count the dynamics see is exact.  Test builds lower kOccMax to exercise it.
+#ifndef PGTG_OCC_MAX
+#define PGTG_OCC_MAX 15
+#endif
+constexpr int kOccMax = PGTG_OCC_MAX;
+static_assert(kOccMax >= 1 && kOccMax <= 15, "4-bit occupancy counters");
+__device__ __forceinline__ int occ_get(const uint8_t* o, int s) { return (o[s >> 1] >> ((s & 1) << 2)) & 15; }
+__device__ __forceinline__ void occ_put(uint8_t* o, int s, int v) {
+  const int sh = (s & 1) << 2;
+  o[s >> 1] = (uint8_t)((o[s >> 1] & ~(15 << sh)) | (v << sh));
+}
+__device__ __forceinline__ void occ_inc(uint8_t* o, int s, bool& sat) {
+  const int v = occ_get(o, s);
+  if (v >= kOccMax) sat = true;
+  else occ_put(o, s, v + 1);
+}
 __device__ __forceinline__ int occ_at(const DevCfg& c, const Plan& pl, const uint8_t* occ, int x, int y) {
   int s = lane_slot(c, pl, x, y);
-  return s < 0 ? 0 : occ[s];
-}
-// returns false on counter overflow (more than 255 cars on one square)
-__device__ __forceinline__ bool occ_inc(uint8_t* occ, int s) {
-  if (occ[s] == 255) return false;
-  occ[s]++;
-  return true;
+  return s < 0 ? 0 : occ_get(occ, s);
 }
 __device__ __forceinline__ int kth_bit(uint32_t m, int k) {
   for (int j = 0; j < k; j++) m &= m - 1u;
@@ -766,9 +779,15 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
     uint32_t ot = plan_otype(p);
     uint32_t CR[3] = {0, 0, 0};  // squares of this tile holding a car
     if ((TR && c.need_car) && occ && ex) {
-      for (int sl = 0; sl < 32; sl++) {
-        if (occ[t * 32 + sl]) {
-          int sq = sT.slot_sq[ex][sl];
+      const uint32_t* ow = reinterpret_cast<const uint32_t*>(occ + t * 16);  // the tile's 32 nibbles
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t wv = ow[q];
+        uint32_t nz = (wv | (wv >> 1) | (wv >> 2) | (wv >> 3)) & 0x11111111u;  // nonzero nibbles
+        while (nz) {
+          const int sl = q * 8 + ((__ffs((int)nz) - 1) >> 2);
+          nz &= nz - 1u;
+          const int sq = sT.slot_sq[ex][sl];
           CR[sq >> 5] |= 1u << (sq & 31);
         }
       }
@@ -886,9 +905,28 @@ __device__ __forceinline__ T sel4(int k, T a0, T a1, T a2, T a3) {
 // the four neighbours, the first admissible one, light and occupancy there) is computed branch-free
 // first; the random draws then go through five draw slots shared by all outcomes (a lane's draws
 // keep numpy's order: delay?, delay length | speed, route | spawner | light, go | profile, route).
+// Exact number of cars on lane slot s while car r leaves it: the cars already moved this tick
+// (survivors [0, w) and respawns [n0 - nnew, n0) of the next bank) and those still to move (r, n0).
+__device__ __noinline__ int recount_slot(const DevCfg& c, const Plan& pl, const CarStore& cs, int cur, int nxt,
+                                         int r, int n0, int w, int nnew, int s) {
+  const int cap = c.car_cap;
+  int n = 0;
+  // three index ranges of two banks (they overlap in index space, not in cars)
+  for (int part = 0; part < 3; part++) {
+    const int bank = part < 2 ? nxt : cur;
+    const int k0 = part == 0 ? 0 : (part == 1 ? n0 - nnew : r + 1);
+    const int k1 = part == 0 ? w : n0;
+    for (int k = k0; k < k1; k++) {
+      const uint32_t w0 = cs.w0[cs.at(bank, cap, k)];
+      n += lane_slot(c, pl, (int)(w0 & 255u), (int)((w0 >> 8) & 255u)) == s ? 1 : 0;
+    }
+  }
+  return n;
+}
+
 __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uint64_t i, const EnvView& v,
-                                         const Plan& pl, uint8_t* occ, const uint16_t* sp, TrafState& ts, Pcg& cr,
-                                         int color, BrakeQuery& bq, uint8_t* hist) {
+                                         const Plan& pl, uint8_t* occ, bool& sat, const uint16_t* sp, TrafState& ts,
+                                         Pcg& cr, int color, BrakeQuery& bq, uint8_t* hist) {
   CarStore cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
   const int cap = c.car_cap, cur = (int)ts.bank, nxt = cur ^ 1;
   const int n0 = (int)ts.n_cars;
@@ -951,7 +989,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
     const uint32_t ex_tg = plan_exits(p_tg);
     const bool tl = plan_otype(p_tg) == 4u && !bit81(sT.wall[ex_tg], tg_q) && bit81(sT.obst[plan_omask(p_tg)], tg_q);
     const int s_tg = tg_t * 32 + sT.li[ex_tg][tg_q];
-    const int occ_tg = dec < 0 ? 0 : occ[s_tg];
+    const int occ_tg = dec < 0 ? 0 : occ_get(occ, s_tg);
     // ---- draws (_should_car_move, route choice / light / following, _spawn_new_car)
     const bool act = delay == 0;
     bool delayed = false, move = false;
@@ -977,7 +1015,10 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
     if (go_try || kind == 3) r4 = pcg_draw(cr, false, 0u);
     if (kind == 3) {
       // _spawn_new_car: choice(car_spawners) -> sorted routes -> profile -> route
-      occ[s_old]--;
+      if (sat && occ_get(occ, s_old) >= kOccMax)
+        occ_put(occ, s_old, min(recount_slot(c, pl, cs, cur, nxt, r, n0, w, nnew, s_old), kOccMax));
+      else
+        occ_put(occ, s_old, occ_get(occ, s_old) - 1);
       int sx = 0, sy = 0;
       if (nsp > 0) {
         const uint32_t code = r3 < (uint64_t)kSpCache ? sp[r3] : S.spawners[r3 * S.n + i];
@@ -998,7 +1039,8 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       cs.id[an] = ts.next_id++;
       nnew++;
       const int s_new = lane_slot(c, pl, sx, sy);
-      if (s_new < 0 || !occ_inc(occ, s_new)) return PGTG_E_UNSUPPORTED;
+      if (s_new < 0) return PGTG_E_UNSUPPORTED;
+      occ_inc(occ, s_new, sat);
       if (bq.tile >= 0 && (s_new >> 5) == bq.tile) {
         bq.n_in++;
         hist[nroute]++;
@@ -1011,9 +1053,12 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       if (moved) {
         nx = x + (dk == 2 ? -1 : (dk == 3 ? 1 : 0));
         ny = y + (dk == 0 ? -1 : (dk == 1 ? 1 : 0));
-        occ[s_old]--;
+        if (sat && occ_get(occ, s_old) >= kOccMax)
+          occ_put(occ, s_old, min(recount_slot(c, pl, cs, cur, nxt, r, n0, w, nnew, s_old), kOccMax));
+        else
+          occ_put(occ, s_old, occ_get(occ, s_old) - 1);
         s_cur = s_tg;
-        if (!occ_inc(occ, s_cur)) return PGTG_E_UNSUPPORTED;
+        occ_inc(occ, s_cur, sat);
         pat = 0;
       } else {
         pat += 1;
@@ -1089,8 +1134,8 @@ struct StepResult {
 
 template <bool TR>
 __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, const Plan& pl,
-                                        int action, StepResult& res, uint8_t* occ, const uint16_t* sp, TrafState& ts,
-                                        uint8_t* hist) {
+                                        int action, StepResult& res, uint8_t* occ, bool& occ_sat, const uint16_t* sp,
+                                        TrafState& ts, uint8_t* hist) {
   res.reward = 0.0;
   res.cost = 0.0;
   if (v.flags & (kFlagTerminated | kFlagTruncated)) return PGTG_E_DONE;
@@ -1107,7 +1152,7 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
   if ((TR && c.need_car) && ts.n_cars > 0) {
     Pcg cr = stream_load(S.car, i);
     STAMP(16);
-    int e = move_cars(c, S, i, v, pl, occ, sp, ts, cr, phase_color(c, v.phase), bq, hist);
+    int e = move_cars(c, S, i, v, pl, occ, occ_sat, sp, ts, cr, phase_color(c, v.phase), bq, hist);
     STAMP(17);
     stream_store_state(S.car, i, cr);
     if (e) return e;
@@ -1419,6 +1464,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
 
   EnvView v{};
   TrafState ts{0, 0, 0, 0};
+  bool occ_sat = false;  // a 4-bit occupancy counter saturated this launch (exact recounts from then on)
   int err = 0;
   if (live) {
     v = rec_load(S.rec, i);
@@ -1441,7 +1487,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   __syncthreads();  // sT ready
   if (live && (TR && c.need_car)) {
     // occupancy counters from the current car positions (one coalesced slot row per car index)
-    for (int w = 0; w < c.nt * 8; w++) traf_w[w] = 0u;
+    for (int w = 0; w < c.nt * 4; w++) traf_w[w] = 0u;  // 16 B of 4-bit counters per tile
     CarStore cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
     const int nc = (int)ts.n_cars;
     for (int k0 = 0; k0 < nc; k0 += 16) {  // 16 independent loads in flight per lane
@@ -1452,7 +1498,8 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       for (int g = 0; g < 16; g++) {
         if (k0 + g < nc) {
           int sl = lane_slot(c, pl, (int)(a16[g] & 255u), (int)((a16[g] >> 8) & 255u));
-          if (sl < 0 || !occ_inc(occ, sl)) err = PGTG_E_UNSUPPORTED;
+          if (sl < 0) err = PGTG_E_UNSUPPORTED;
+          else occ_inc(occ, sl, occ_sat);
         }
       }
     }
@@ -1472,7 +1519,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (live) {
     if (mode == MODE_STEP) {
       StepResult res{0.0, 0.0, 0u};
-      if (!err) err = env_step<TR>(c, S, i, v, pl, actions[i], res, occ, sp_l, ts, hist);
+      if (!err) err = env_step<TR>(c, S, i, v, pl, actions[i], res, occ, occ_sat, sp_l, ts, hist);
       const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
       if (out.reward) out.reward[i] = res.reward;
       if (out.cost) out.cost[i] = res.cost;
@@ -1941,8 +1988,8 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
     if (cap < 1) cap = 1;
     c.car_cap = cap;
     c.max_spawners = c.nt * 5;
-    // k_env: occupancy counters (nt * 32 lane slots, u8) then the spawner cache
-    c.sp_cache_off = c.nt * 32;
+    // k_env: occupancy counters (nt * 32 lane slots, 4 bit) then the spawner cache
+    c.sp_cache_off = c.nt * 16;
     c.traf_bytes = c.sp_cache_off + 2 * kSpCache;
     // k_traffic: Floyd output (u16 x cap), seen bits of the spawnable squares (<= nt * 32), column prefix
     c.rs_seen_off = ((2 * cap + 3) / 4) * 4;
@@ -2132,7 +2179,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     // sub-batch so that two workgroups share a CU's 160 KiB of LDS when the counters allow it.
     // Small batches: fewer envs per workgroup so that every CU gets one (a workgroup's time is the
     // slowest of its lanes' serial chains); traffic: 64 (LDS).
-    int envs = c.need_car ? 64
+    int envs = c.need_car ? 128
              : n_envs <= (uint64_t)8 * 1024 ? 16
              : n_envs <= (uint64_t)16 * 1024 ? 32
              : n_envs <= (uint64_t)64 * 1024 ? 64
@@ -2141,6 +2188,21 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     if (envs != 16 && envs != 32 && envs != 64 && envs != 128 && envs != kBlock) envs = kBlock;
     while (envs > 16 && lds_bytes(lds_layout(c, envs)) + sizeof(Tables) > 150 * 1024) envs /= 2;
     h->L = lds_layout(c, envs);
+    if (c.need_car) {
+      // traffic: the most envs per workgroup (<= 128) for which two workgroups share a CU's LDS
+      // after shrinking the observation sub-batch; else the largest that fits at all
+      auto shrink = [&](Lds l) {
+        while (l.sub_envs > 8 && lds_bytes(l) + sizeof(Tables) > 80 * 1024) {
+          l.sub_envs /= 2;
+          l.stream_words = l.sub_envs * l.seg_words + 2;
+        }
+        return l;
+      };
+      Lds best = shrink(lds_layout(c, envs));
+      while (best.envs > 16 && lds_bytes(best) + sizeof(Tables) > 80 * 1024) best = shrink(lds_layout(c, best.envs / 2));
+      if (lds_bytes(best) + sizeof(Tables) > 80 * 1024) best = shrink(lds_layout(c, envs));
+      h->L = best;
+    }
     if (!c.need_car && h->L.envs == kBlock) {
       // Large batches: when the grid needs more workgroups per CU than fit the LDS (up to the 4 that
       // the registers allow), observe in sub-batches so that the whole grid runs in one round.
@@ -2160,10 +2222,6 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
       }
     }
     if (c.need_car) {
-      while (h->L.sub_envs > 8 && lds_bytes(h->L) + sizeof(Tables) > 80 * 1024) {
-        h->L.sub_envs /= 2;
-        h->L.stream_words = h->L.sub_envs * h->L.seg_words + 2;
-      }
       // k_traffic: per-lane plan + reset scratch
       h->kt_plan_dw = odd_up((c.nt + 1) / 2);
       h->kt_rs_dw = odd_up(c.rs_bytes / 4);
