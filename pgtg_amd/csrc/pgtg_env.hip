@@ -296,13 +296,15 @@ __device__ __forceinline__ M expand(M R, M hN, M hE, M hS, M hW, int w) {
 // component is exhausted first, in which case s-g broke iff exactly one of s, g lies in it.
 template <typename M>
 __device__ __forceinline__ bool still_connected(M hN, M hE, M hS, M hW, int w, int a, int b, int s, int g) {
+  // Two expansions per side between checks: the sets only grow, so meeting and exhaustion are
+  // still detected (at most one expansion late) with half the loop control of a step-wise loop.
   M Ra = (M)1 << a, Rb = (M)1 << b;
   for (;;) {
-    M Na = expand<M>(Ra, hN, hE, hS, hW, w);
-    M Nb = expand<M>(Rb, hN, hE, hS, hW, w);
+    const M Ma = expand<M>(Ra, hN, hE, hS, hW, w), Mb = expand<M>(Rb, hN, hE, hS, hW, w);
+    const M Na = expand<M>(Ma, hN, hE, hS, hW, w), Nb = expand<M>(Mb, hN, hE, hS, hW, w);
     if (Na & Nb) return true;
-    if (Na == Ra) return ((Ra >> s) & 1) == ((Ra >> g) & 1);
-    if (Nb == Rb) return ((Rb >> s) & 1) == ((Rb >> g) & 1);
+    if (Na == Ma) return ((Na >> s) & 1) == ((Na >> g) & 1);
+    if (Nb == Mb) return ((Nb >> s) & 1) == ((Nb >> g) & 1);
     Ra = Na;
     Rb = Nb;
   }
@@ -319,13 +321,28 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, 
   EdgeBits<NW> L;
   L.init(c.n_edges);
   int nrem = c.n_edges, count = c.n_edges;
-  while (count > c.keep && nrem > 0) {
-    const int k = (int)pcg_draw(r, true, (uint32_t)nrem);  // nrem >= 2: always draws
+  if (!(count > c.keep && nrem > 0)) return;
+  // The candidate sequence (draw -> list index -> edge pair) does not depend on whether earlier
+  // removals were undone, so the next candidate is drawn while the current one is tested (two
+  // independent dependency chains per iteration); the speculative draw is rolled back on exit.
+  auto draw_candidate = [&](int n) {
+    const int k = (int)pcg_draw(r, true, (uint32_t)n);  // n >= 2: always draws
     const int e = L.select(k);
     const uint32_t pk = sT.epk[e];
     L.clear(e);
     L.clear((int)(pk >> 24));
-    nrem -= 2;
+    return pk;
+  };
+  uint32_t pk = draw_candidate(nrem);
+  nrem -= 2;
+#ifdef PGTG_STAMPS
+  unsigned long long dbg_bfs = 0, dbg_iters = 0;
+#endif
+  for (;;) {
+    Pcg r_before = r;
+    uint32_t pk_next = 0;
+    const bool more = nrem > 0;
+    if (more) pk_next = draw_candidate(nrem);
     const int a = (int)(pk & 255u), b = (int)((pk >> 8) & 255u), d = (int)((pk >> 16) & 255u);
     const M ma = (M)1 << a, mb = (M)1 << b;
     const M sN = hN, sE = hE, sS = hS, sW = hW;
@@ -344,11 +361,30 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, 
       cyc = lf || rt;
     }
     count -= 2;
+#ifdef PGTG_STAMPS
+    const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
+#endif
     if (!cyc && !still_connected<M>(hN, hE, hS, hW, w, a, b, st_t, gl_t)) {
       hN = sN; hE = sE; hS = sS; hW = sW;
       count += 2;
     }
+#ifdef PGTG_STAMPS
+    dbg_bfs += __builtin_amdgcn_s_memtime() - tb0;
+    dbg_iters++;
+#endif
+    if (!(count > c.keep && more)) {
+      r = r_before;  // the reference stops drawing here
+      break;
+    }
+    pk = pk_next;
+    nrem -= 2;
   }
+#ifdef PGTG_STAMPS
+  if ((threadIdx.x & 63) == 0) {  // lane 0's loop: cycles in the connectivity test, iterations
+    g_stamps[((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 32 + 26) & ((1 << 21) - 1)] = dbg_bfs;
+    g_stamps[((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 32 + 27) & ((1 << 21) - 1)] = dbg_iters;
+  }
+#endif
 }
 
 template <int NW>
@@ -459,40 +495,58 @@ __device__ __forceinline__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* 
 
 // parse_map_object's shortest path (graph-theory Dijkstra == FIFO BFS, neighbours N,E,S,W)
 // -> subgoal directions in the plan; returns the path length (num_subgoals) or 0.
-__device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, uint8_t* q, uint8_t* par, int s, int g) {
-  const int w = c.tw, h = c.th;
-  uint64_t seen = 1ull << s;
-  int qh = 0, qt = 0;
-  q[qt++] = (uint8_t)s;
-  par[s] = 255;
-  bool found = false;
-  while (qh < qt) {
-    int v = q[qh++];
-    if (v == g) {
-      found = true;
-      break;
-    }
-    int x = v % w, y = v / w;
-    uint32_t e = plan_exits(plan[v]);
-    int nb[4] = {v - w, v + 1, v + w, v - 1};
-    bool ok[4] = {(e & 1u) && y > 0, (e & 2u) && x < w - 1, (e & 4u) && y < h - 1, (e & 8u) && x > 0};
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-      if (ok[d] && !((seen >> nb[d]) & 1ull)) {
-        seen |= 1ull << nb[d];
-        par[nb[d]] = (uint8_t)v;
-        q[qt++] = (uint8_t)nb[d];
-      }
-    }
+// parse_map_object's shortest_path (pgtg/parser.py:30-32, 244-306) on the tile exit graph, written as
+// bit-parallel BFS layers from the goal (masks of type M) plus a greedy walk from the start that
+// takes the first of north, east, south, west leading one layer closer.  That walk is the path a
+// FIFO BFS with neighbour order N, E, S, W reconstructs (the assumed graph-theory tie-break,
+// DESIGN.md section 2; checked against the queue BFS on random grids).  While the layers grow, the
+// tiles whose N/E/S/W neighbour lies one layer closer are collected as masks, so the walk is
+// register arithmetic.  Marks the direction to the next tile on every path tile but the goal's;
+// returns the number of path tiles (0: unreachable).
+template <typename M>
+__device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, int s, int g) {
+  const int w = c.tw;
+  M hN = 0, hE = 0, hS = 0, hW = 0;
+  for (int t = 0; t < c.nt; t++) {
+    const M e = (M)plan_exits(plan[t]);
+    hN |= (e & 1) << t;
+    hE |= ((e >> 1) & 1) << t;
+    hS |= ((e >> 2) & 1) << t;
+    hW |= ((e >> 3) & 1) << t;
   }
-  if (!found) return 0;
-  int len = 1, ch = g;
-  while (par[ch] != 255) {
-    int p = par[ch];
-    int d = (ch == p - w) ? 0 : (ch == p + 1) ? 1 : (ch == p + w) ? 2 : 3;
-    plan[p] = (uint16_t)((plan[p] & ~(7u << 11)) | (uint32_t)(d + 1) << 11);
-    ch = p;
+  hN &= (M)c.h0[0];  // interior exits only: border exits lead off the map
+  hE &= (M)c.h0[1];
+  hS &= (M)c.h0[2];
+  hW &= (M)c.h0[3];
+  STAMP(24);
+  M vis = (M)1 << g, front = vis;
+  M cN = 0, cE = 0, cS = 0, cW = 0;  // tiles with a neighbour one layer closer, per direction
+  while (!((vis >> s) & 1)) {
+    const M nx = expand<M>(front, hN, hE, hS, hW, w) & ~vis;
+    if (!nx) return 0;
+    cN |= nx & hN & (front << w);
+    cE |= nx & hE & (front >> 1);
+    cS |= nx & hS & (front >> w);
+    cW |= nx & hW & (front << 1);
+    vis |= nx;
+    front = nx;
+  }
+  STAMP(25);
+  M pN = 0, pE = 0, pS = 0, pW = 0;
+  int v = s, len = 1;
+  while (v != g) {
+    const M b = (M)1 << v;
+    if (cN & b) { pN |= b; v -= w; }
+    else if (cE & b) { pE |= b; v += 1; }
+    else if (cS & b) { pS |= b; v += w; }
+    else { pW |= b; v -= 1; }
     len++;
+  }
+  for (M m = pN | pE | pS | pW; m; m &= m - 1) {
+    const int t = __builtin_ctzll((uint64_t)m);
+    const M b = (M)1 << t;
+    const uint32_t d = (pN & b) ? 1u : (pE & b) ? 2u : (pS & b) ? 3u : 4u;
+    plan[t] = (uint16_t)((plan[t] & ~(7u << 11)) | d << 11);
   }
   return len;
 }
@@ -645,7 +699,7 @@ __device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uin
   }
   v.sg = (uint32_t)st_t | (uint32_t)st_d << 8 | (uint32_t)gl_t << 16 | (uint32_t)gl_d << 24;
   STAMP(10);
-  int len = compile_path(c, plan, q, par, st_t, gl_t);
+  int len = c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t);
   STAMP(11);
   v.used = 0;
   v.path_len = (uint32_t)len;

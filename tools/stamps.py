@@ -20,7 +20,7 @@ from pgtg_amd.vector import PGTGVecEnv  # noqa: E402
 SLOTS = 32
 PHASES = ["stage", "step", "final", "reset", "store", "obs"]
 SUB = {"cars": (16, 17), "braking": (17, 18), "reset.seed": (8, 9), "reset.generate": (9, 10),
-       "reset.compile": (10, 11), "reset.start": (11, 12), "gen.start_goal": (9, 13), "gen.edge_init": (13, 14),
+       "reset.compile": (10, 11), "path.masks": (10, 24), "path.bfs": (24, 25), "path.walk": (25, 11), "reset.start": (11, 12), "gen.start_goal": (9, 13), "gen.edge_init": (13, 14),
        "gen.removal": (14, 15), "gen.tiles": (15, 10), "traf.spawners": (19, 20), "traf.floyd": (20, 21),
        "traf.shuffle": (21, 22), "traf.create": (22, 23)}
 CASES = {"cfg2": (4096, dict(random_map_width=3, random_map_height=3)),
@@ -57,4 +57,8 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
         if ok.any():
             out[n] = (int((st[ok, b] - st[ok, a]).mean()), round(float(ok.mean()), 2))
     print("  sub-phases (mean cycles, fraction of waves):", out, flush=True)
+    okr = (st[:, 14] >= lo) & (st[:, 14] <= hi) & (st[:, 27] > 0) & (st[:, 27] < 1000)
+    if okr.any():
+        print("  removal loop (lane 0): iterations", round(float(st[okr, 27].mean()), 1), "max", int(st[okr, 27].max()),
+              "connectivity-test cycles", int(st[okr, 26].mean()), flush=True)
     env.close()
