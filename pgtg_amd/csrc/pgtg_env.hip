@@ -1429,6 +1429,7 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.sub_envs = sub > envs ? envs : (sub < 1 ? 1 : sub);
   l.stream_words = l.sub_envs * l.seg_words + 2;
   l.spread = c.need_car ? 1 : 0;
+  if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);  // tuning knob
   return l;
 }
 __host__ inline size_t lds_bytes(const Lds& l) {
