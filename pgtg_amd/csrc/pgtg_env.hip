@@ -1355,14 +1355,16 @@ __device__ __forceinline__ uint32_t udiv_f(uint32_t x, uint32_t d, float inv) {
   return q;
 }
 
+// Threads [t0, t0 + nthr) of the workgroup share the chunks (all of them, or helper waves).
 __device__ __forceinline__ void write_obs(uint8_t* __restrict__ dst, uint32_t cnt, uint32_t WW, uint32_t MW,
-                                          uint32_t C, const uint32_t* st, const uint8_t* sel) {
+                                          uint32_t C, const uint32_t* st, const uint8_t* sel, int t0 = 0,
+                                          int nthr = kBlock) {
   const uint32_t OB = C * WW, total = cnt * OB;
   const uintptr_t a0 = (uintptr_t)dst;
   const uintptr_t c0 = a0 & ~(uintptr_t)15;
   const uint32_t nchunks = (uint32_t)((a0 + total - c0 + 15) >> 4);
   const float invWW = 1.0f / (float)WW, invOB = 1.0f / (float)OB;
-  for (uint32_t ch = threadIdx.x; ch < nchunks; ch += blockDim.x) {
+  for (uint32_t ch = (uint32_t)((int)threadIdx.x - t0); ch < nchunks; ch += (uint32_t)nthr) {
     const int r = (int)((intptr_t)(c0 + ((uintptr_t)ch << 4)) - (intptr_t)a0);  // > -16
     const uint32_t lo = r < 0 ? 0u : (uint32_t)r;
     const uint32_t hi = min((uint32_t)(r + 15), total - 1u);
@@ -1591,6 +1593,10 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (has_slot) sel[slot] = my_sel;
   STAMP(2);
   const bool single = L.sub_envs >= nb;  // the whole workgroup's image fits: build once, rebuild resets
+  // waves without env slots (workgroups of fewer than 256 unspread envs) write the terminal
+  // observations while the env waves run their resets
+  const int env_threads = (L.spread || L.envs >= kBlock) ? kBlock : ((L.envs + 63) / 64) * 64;
+  const bool helpers = single && env_threads < kBlock;
   const int n_final = __syncthreads_count(my_sel == 1);
   const bool want_final = mode == MODE_STEP && n_final && (out.final_obs || out.final_position || out.final_velocity);
   if (single) {
@@ -1599,8 +1605,10 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       build_obs<TR>(c, S, pl, v, st + slot * L.seg_words, oi, occ);
       write_small_outputs(c, out, i, v, oi, my_sel == 1);
     }
+    STAMP(28);
     __syncthreads();
-    if (want_final && out.final_obs)
+    STAMP(29);
+    if (want_final && out.final_obs && !helpers)
       write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
                 (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel);
   } else if (want_final) {
@@ -1611,6 +1619,9 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   bool tr_push = false;
   const int n_resets = __syncthreads_count(reset_now);
   if (tid == 0 && n_resets) atomicAdd(&S.counters[1], (unsigned long long)n_resets);
+  if (helpers && want_final && out.final_obs && tid >= env_threads)
+    write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
+              (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel, env_threads, kBlock - env_threads);
   if (reset_now) {
     int e2 = env_reset<TR>(c, S, i, v, pl.p, q, par, ts);
     if (e2) err = e2;
@@ -1644,12 +1655,15 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   }
   STAMP(5);
   if (single) {
+    if (helpers) __syncthreads();  // the terminal observations are written before slots are rebuilt
     if (reset_now) {
       ObsInfo oi;
       build_obs<TR>(c, S, pl, v, st + slot * L.seg_words, oi, nullptr);  // cars come from k_traffic
       write_small_outputs(c, out, i, v, oi, false);
     }
+    STAMP(30);
     __syncthreads();
+    STAMP(31);
     if (out.obs)
       write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
                 (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, nullptr);

@@ -22,7 +22,9 @@ PHASES = ["stage", "step", "final", "reset", "store", "obs"]
 SUB = {"cars": (16, 17), "braking": (17, 18), "reset.seed": (8, 9), "reset.generate": (9, 10),
        "reset.compile": (10, 11), "path.masks": (10, 24), "path.bfs": (24, 25), "path.walk": (25, 11), "reset.start": (11, 12), "gen.start_goal": (9, 13), "gen.edge_init": (13, 14),
        "gen.removal": (14, 15), "gen.tiles": (15, 10), "traf.spawners": (19, 20), "traf.floyd": (20, 21),
-       "traf.shuffle": (21, 22), "traf.create": (22, 23)}
+       "traf.shuffle": (21, 22), "traf.create": (22, 23),
+       "final.build": (2, 28), "final.barrier": (28, 29), "final.write": (29, 3),
+       "obs.rebuild": (5, 30), "obs.barrier": (30, 31), "obs.write": (31, 6)}
 CASES = {"cfg2": (4096, dict(random_map_width=3, random_map_height=3)),
          "cfg5": (131072, dict(random_map_width=5, random_map_height=5)),
          "cfg3": (65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5))}
