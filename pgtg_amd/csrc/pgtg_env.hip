@@ -674,7 +674,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
 // The full per-env reset.  `key` = spawn counter (5 children per episode).  Returns 0 or -code.
 template <bool TR>
 __device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, uint16_t* plan,
-                                         uint8_t* q, uint8_t* par, TrafState& ts) {
+                                         TrafState& ts) {
   STAMP(8);
   uint64_t seed = S.seed[i];
   SeedPool sp = ss_pool(seed);
@@ -1407,13 +1407,14 @@ __device__ __forceinline__ void write_obs(uint8_t* __restrict__ dst, uint32_t cn
 struct Lds {
   int envs;            // envs per workgroup (<= kBlock); lanes >= envs only help with the writes
   int plan_stride_dw;  // per-lane plan words (odd)
-  int scratch_dw;      // per-lane BFS scratch words (odd)
+  int scratch_dw;      // per-env reset hand-over words (odd): spawn in; position, sg, path length out
   int traf_dw;         // per-lane traffic region words (occupancy counters / reset scratch), odd or 0
   int hist_dw;         // per-lane route histogram words for the braking rules, odd or 0
   int seg_words;       // per-env observation words (n_channels * mask_words)
   int sub_envs;        // envs per observation sub-batch (== envs when they all fit)
   int stream_words;    // observation image words (+2 pad)
   int spread;          // env slots spread over the four waves (traffic: long per-lane chains)
+  int compact;         // resets run on dense lanes (wave 0 first) instead of on their env's lane
 };
 
 __host__ __device__ inline int odd_up(int x) { return x | 1; }
@@ -1422,7 +1423,7 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   Lds l;
   l.envs = envs;
   l.plan_stride_dw = odd_up((c.nt + 1) / 2);
-  l.scratch_dw = c.need_car ? 0 : odd_up((2 * c.nt + 3) / 4);  // with traffic: inside the counters
+  l.scratch_dw = c.need_car ? 0 : 3;  // with traffic: inside the (by then dead) occupancy counters
   l.traf_dw = c.need_car ? odd_up(c.traf_bytes / 4) : 0;
   l.hist_dw = c.n_rules > 0 ? 5 : 0;
   l.seg_words = c.n_channels * c.mask_words;
@@ -1432,11 +1433,13 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.stream_words = l.sub_envs * l.seg_words + 2;
   l.spread = c.need_car ? 1 : 0;
   if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);  // tuning knob
+  l.compact = 1;
+  if (const char* e = getenv("PGTG_COMPACT")) l.compact = atoi(e);  // tuning knob
   return l;
 }
 __host__ inline size_t lds_bytes(const Lds& l) {
   return (size_t)4 * ((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
-         kBlock;
+         kBlock + 32;
 }
 
 enum { MODE_STEP = 0, MODE_RESET_SEEDED = 1, MODE_RESET_UNSEEDED = 2, MODE_OBSERVE = 3 };
@@ -1506,18 +1509,18 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   const bool live = has_slot && slot < nb;
   const int my_slot = slot;
   uint32_t* plan_w = lds + my_slot * L.plan_stride_dw;
-  uint32_t* scr_w = lds + L.envs * L.plan_stride_dw + my_slot * L.scratch_dw;
   uint32_t* traf_w = lds + L.envs * (L.plan_stride_dw + L.scratch_dw) + my_slot * L.traf_dw;
   uint32_t* hist_w = lds + L.envs * (L.plan_stride_dw + L.scratch_dw + L.traf_dw) + my_slot * L.hist_dw;
   uint32_t* st = lds + L.envs * (L.plan_stride_dw + L.scratch_dw + L.traf_dw + L.hist_dw);
   uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
+  uint64_t* wmask = reinterpret_cast<uint64_t*>(sel + kBlock);     // [4] reset ballot per wave
+  const int xf_off = L.envs * L.plan_stride_dw + ((TR && c.need_car) ? L.envs * L.scratch_dw : 0);
+  const int xf_dw = (TR && c.need_car) ? L.traf_dw : L.scratch_dw;
+  uint32_t* xf = lds + xf_off + my_slot * xf_dw;  // reset hand-over words
   uint8_t* occ = reinterpret_cast<uint8_t*>(traf_w);
   uint16_t* sp_l = reinterpret_cast<uint16_t*>(occ + c.sp_cache_off);  // first spawners of the list
   uint8_t* hist = reinterpret_cast<uint8_t*>(hist_w);
   Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
-  // the map reset's BFS scratch reuses the occupancy counters, which are dead by then
-  uint8_t* q = (TR && c.need_car) ? occ : reinterpret_cast<uint8_t*>(scr_w);
-  uint8_t* par = q + c.nt;
 
   EnvView v{};
   TrafState ts{0, 0, 0, 0};
@@ -1593,37 +1596,95 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (has_slot) sel[slot] = my_sel;
   STAMP(2);
   const bool single = L.sub_envs >= nb;  // the whole workgroup's image fits: build once, rebuild resets
-  // waves without env slots (workgroups of fewer than 256 unspread envs) write the terminal
-  // observations while the env waves run their resets
-  const int env_threads = (L.spread || L.envs >= kBlock) ? kBlock : ((L.envs + 63) / 64) * 64;
-  const bool helpers = single && env_threads < kBlock;
+  const bool reset_now = my_sel != 0;
+  if (L.compact) {  // the workgroup's resets, in wave order, go to threads 0 .. n_resets-1
+    const uint64_t m = __ballot(reset_now);
+    if ((tid & 63) == 0) wmask[tid >> 6] = m;
+  }
   const int n_final = __syncthreads_count(my_sel == 1);
   const bool want_final = mode == MODE_STEP && n_final && (out.final_obs || out.final_position || out.final_velocity);
+  int n_resets = 0, wslot = -1;
+  if (L.compact) {
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; w++) {
+      const uint64_t m = wmask[w];
+      const int cw = __popcll(m);
+      if (tid >= n_resets && tid < n_resets + cw) wslot = w * per_wave + select64(m, tid - n_resets);
+      n_resets += cw;
+    }
+  }
+  // threads without a reset (compacted), or waves without env slots (workgroups of fewer than 256
+  // unspread envs), write the terminal observations while the resets run
+  const int t_help = L.compact ? ((n_resets + 63) / 64) * 64
+                               : ((L.spread || L.envs >= kBlock) ? kBlock : ((L.envs + 63) / 64) * 64);
+  const bool helpers = single && t_help < kBlock;
   if (single) {
     if (live && (my_sel != 2)) {
       ObsInfo oi;
       build_obs<TR>(c, S, pl, v, st + slot * L.seg_words, oi, occ);
       write_small_outputs(c, out, i, v, oi, my_sel == 1);
     }
+    if (L.compact && reset_now) xf[0] = v.spawn;  // after the terminal image read the counters
     STAMP(28);
     __syncthreads();
     STAMP(29);
     if (want_final && out.final_obs && !helpers)
       write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
                 (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel);
-  } else if (want_final) {
-    obs_pass<TR>(c, S, pl, v, out, out.final_obs, env0, nb, my_sel == 1, true, sel, st, L, occ, slot);
+  } else {
+    if (want_final) obs_pass<TR>(c, S, pl, v, out, out.final_obs, env0, nb, my_sel == 1, true, sel, st, L, occ, slot);
+    if (L.compact) {
+      if (reset_now) xf[0] = v.spawn;
+      __syncthreads();
+    }
   }
   STAMP(3);
-  const bool reset_now = my_sel != 0;
   bool tr_push = false;
-  const int n_resets = __syncthreads_count(reset_now);
+  if (!L.compact) n_resets = __syncthreads_count(reset_now);
   if (tid == 0 && n_resets) atomicAdd(&S.counters[1], (unsigned long long)n_resets);
-  if (helpers && want_final && out.final_obs && tid >= env_threads)
+  if (helpers && want_final && out.final_obs && tid >= t_help)
     write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
-              (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel, env_threads, kBlock - env_threads);
-  if (reset_now) {
-    int e2 = env_reset<TR>(c, S, i, v, pl.p, q, par, ts);
+              (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel, t_help, kBlock - t_help);
+  if (L.compact) {
+    if (wslot >= 0) {
+      uint32_t* xw = lds + xf_off + wslot * xf_dw;
+      uint32_t* pw = lds + wslot * L.plan_stride_dw;
+      const uint64_t iw = env0 + wslot;
+      EnvView vv{};
+      vv.spawn = xw[0];
+      TrafState tw{0, 0, 0, 0};
+      const int e2 = env_reset<TR>(c, S, iw, vv, reinterpret_cast<uint16_t*>(pw), tw);
+      uint4* dstp = reinterpret_cast<uint4*>(S.plan + iw * (uint64_t)c.plan_stride);
+      for (int k = 0; k < c.plan_stride / 8; k++) {
+        uint32_t wv[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) wv[j] = (k * 4 + j < L.plan_stride_dw) ? pw[k * 4 + j] : 0u;
+        dstp[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      }
+      xw[0] = ((uint32_t)vv.px & 0xffffu) | ((uint32_t)vv.py << 16);
+      xw[1] = vv.sg;
+      xw[2] = vv.path_len | (uint32_t)(-e2) << 16;
+    }
+    __syncthreads();  // hand-over words ready (and the terminal observations written)
+    if (reset_now) {  // env_reset's state on the env's own lane
+      const uint32_t x0 = xf[0], x2 = xf[2];
+      v.px = (int)(int16_t)(x0 & 0xffffu);
+      v.py = (int)(int16_t)(x0 >> 16);
+      v.sg = xf[1];
+      v.path_len = x2 & 0xffffu;
+      v.spawn += 5u;
+      v.used = 0;
+      v.flags = 0;
+      v.phase = 0;
+      v.elapsed = 0;
+      v.vx = v.vy = 0;
+      const int e2 = -(int)(x2 >> 16);
+      if (e2) err = e2;
+      tr_push = (TR && c.need_car) && e2 == 0;
+      if ((TR && c.need_car) && e2 == 0) ts = TrafState{0, 0, 0, 0};
+    }
+  } else if (reset_now) {
+    int e2 = env_reset<TR>(c, S, i, v, pl.p, ts);
     if (e2) err = e2;
     tr_push = (TR && c.need_car) && e2 == 0;
     uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
@@ -1655,7 +1716,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   }
   STAMP(5);
   if (single) {
-    if (helpers) __syncthreads();  // the terminal observations are written before slots are rebuilt
+    if (helpers && !L.compact) __syncthreads();  // the terminal observations are written before slots are rebuilt
     if (reset_now) {
       ObsInfo oi;
       build_obs<TR>(c, S, pl, v, st + slot * L.seg_words, oi, nullptr);  // cars come from k_traffic
