@@ -285,10 +285,19 @@ struct EdgeBits {
   }
 };
 
-// One BFS step on the symmetric tile graph given by the four exit masks.
+// One BFS step on the tile graph given by the four exit masks (tile t reaches its neighbours in
+// the directions of its exits).
 template <typename M>
 __device__ __forceinline__ M expand(M R, M hN, M hE, M hS, M hW, int w) {
   return R | ((R & hN) >> w) | ((R & hS) << w) | ((R & hE) << 1) | ((R & hW) >> 1);
+}
+// The same on a symmetric graph (t has a south exit iff t+w has a north exit, ...): "R's tiles with
+// a south exit, moved one row down" equals "R moved one row down, restricted to tiles with a north
+// exit" -- one shift and one and-or per direction, the four shifts independent of each other.
+template <typename M>
+__device__ __forceinline__ M expand_sym(M R, M hN, M hE, M hS, M hW, int w) {
+  const M dn = R << w, up = R >> w, rt = R << 1, lf = R >> 1;
+  return R | (dn & hN) | (up & hS) | (rt & hW) | (lf & hE);
 }
 
 // After deleting edge a-b from a graph in which start s and goal g were connected: are they still?
@@ -296,18 +305,25 @@ __device__ __forceinline__ M expand(M R, M hN, M hE, M hS, M hW, int w) {
 // component is exhausted first, in which case s-g broke iff exactly one of s, g lies in it.
 template <typename M>
 __device__ __forceinline__ bool still_connected(M hN, M hE, M hS, M hW, int w, int a, int b, int s, int g) {
+#ifdef PGTG_ABL_NOBFS  // diagnostic timing build only
+  return ((hN ^ hS) >> a) & 1;
+#endif
   // Two expansions per side between checks: the sets only grow, so meeting and exhaustion are
   // still detected (at most one expansion late) with half the loop control of a step-wise loop.
+  // One exit condition keeps the loop's mask bookkeeping short.
   M Ra = (M)1 << a, Rb = (M)1 << b;
-  for (;;) {
-    const M Ma = expand<M>(Ra, hN, hE, hS, hW, w), Mb = expand<M>(Rb, hN, hE, hS, hW, w);
-    const M Na = expand<M>(Ma, hN, hE, hS, hW, w), Nb = expand<M>(Mb, hN, hE, hS, hW, w);
-    if (Na & Nb) return true;
-    if (Na == Ma) return ((Na >> s) & 1) == ((Na >> g) & 1);
-    if (Nb == Mb) return ((Nb >> s) & 1) == ((Nb >> g) & 1);
+  bool done, res;
+  do {
+    const M Ma = expand_sym<M>(Ra, hN, hE, hS, hW, w), Mb = expand_sym<M>(Rb, hN, hE, hS, hW, w);
+    const M Na = expand_sym<M>(Ma, hN, hE, hS, hW, w), Nb = expand_sym<M>(Mb, hN, hE, hS, hW, w);
+    const bool meet = (Na & Nb) != 0, exa = Na == Ma, exb = Nb == Mb;
+    const M X = exa ? Na : Nb;
+    res = meet || (((X >> s) ^ (X >> g)) & 1) == 0;
+    done = meet || exa || exb;
     Ra = Na;
     Rb = Nb;
-  }
+  } while (!done);
+  return res;
 }
 
 // generate_map_graph's edge-removal loop (map_generator.py:218-264) on exit masks of type M
@@ -325,41 +341,43 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, 
   // The candidate sequence (draw -> list index -> edge pair) does not depend on whether earlier
   // removals were undone, so the next candidate is drawn while the current one is tested (two
   // independent dependency chains per iteration); the speculative draw is rolled back on exit.
-  auto draw_candidate = [&](int n) {
+  // The next candidate's edge-table read overlaps the test; its reverse entry leaves the list at
+  // the end of the iteration, before the following draw.
+  auto draw_edge = [&](int n) {
     const int k = (int)pcg_draw(r, true, (uint32_t)n);  // n >= 2: always draws
+#ifdef PGTG_ABL_NOSELECT  // diagnostic timing build only
+    const int e = k;
+#else
     const int e = L.select(k);
-    const uint32_t pk = sT.epk[e];
+#endif
     L.clear(e);
-    L.clear((int)(pk >> 24));
-    return pk;
+    return e;
   };
-  uint32_t pk = draw_candidate(nrem);
+  uint32_t pk = sT.epk[draw_edge(nrem)];
+  L.clear((int)(pk >> 24));
   nrem -= 2;
 #ifdef PGTG_STAMPS
   unsigned long long dbg_bfs = 0, dbg_iters = 0;
 #endif
   for (;;) {
     Pcg r_before = r;
-    uint32_t pk_next = 0;
-    const bool more = nrem > 0;
-    if (more) pk_next = draw_candidate(nrem);
-    const int a = (int)(pk & 255u), b = (int)((pk >> 8) & 255u), d = (int)((pk >> 16) & 255u);
-    const M ma = (M)1 << a, mb = (M)1 << b;
+    const bool more = nrem > 0;  // uniform: every lane is in the same iteration
+    int e_next = 0;
+    if (more) e_next = draw_edge(nrem);
+    const uint32_t pk_next = sT.epk[e_next];
+    // remove edge a-b (horizontal: a left of b; vertical: a above b), branch-free
+    const int a = (int)(pk & 255u), b = (int)((pk >> 8) & 255u);
+    const bool hz = ((pk >> 16) & 255u) == 1u;
+    const M ma = (M)1 << a, mb = (M)1 << b, mab = ma | mb;
     const M sN = hN, sE = hE, sS = hS, sW = hW;
-    bool cyc;
-    if (d == 1) {  // horizontal a | b
-      hE &= ~ma;
-      hW &= ~mb;
-      const bool up = (hN & ma) && (hN & mb) && (hE & (ma >> w));
-      const bool dn = (hS & ma) && (hS & mb) && (hE & (ma << w));
-      cyc = up || dn;
-    } else {       // vertical a over b
-      hS &= ~ma;
-      hN &= ~mb;
-      const bool lf = (hW & ma) && (hW & mb) && (hS & (ma >> 1));
-      const bool rt = (hE & ma) && (hE & mb) && (hS & (ma << 1));
-      cyc = lf || rt;
-    }
+    hE &= ~(hz ? ma : (M)0);
+    hW &= ~(hz ? mb : (M)0);
+    hS &= ~(hz ? (M)0 : ma);
+    hN &= ~(hz ? (M)0 : mb);
+    // an intact unit square through a and b on either side keeps everything connected
+    const M P1 = hz ? hN : hW, P2 = hz ? hS : hE, F = hz ? hE : hS;
+    const int off = hz ? w : 1;
+    const bool cyc = ((P1 & mab) == mab && (F & (ma >> off))) || ((P2 & mab) == mab && (F & (ma << off)));
     count -= 2;
 #ifdef PGTG_STAMPS
     const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
@@ -376,6 +394,7 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, 
       r = r_before;  // the reference stops drawing here
       break;
     }
+    L.clear((int)(pk_next >> 24));
     pk = pk_next;
     nrem -= 2;
   }
@@ -1736,6 +1755,45 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   STAMP(6);
 }
 
+#ifdef PGTG_STAMPS
+__global__ void __launch_bounds__(kBlock) k_gen_bench(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
+                                                      DevState S, int reps, int active, int pdw) {
+  extern __shared__ uint32_t lds[];
+  const DevCfg& c = *cfg;
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
+    uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
+    for (int k = threadIdx.x; k < (int)(offsetof(Tables, lanes) / 4); k += blockDim.x) dstt[k] = src[k];
+  }
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  uint16_t* plan = reinterpret_cast<uint16_t*>(lds + threadIdx.x * pdw);
+  unsigned long long tg = 0, tc = 0;
+  uint32_t chk = 0;
+  if ((threadIdx.x & 63) < active && i < S.n) {
+    SeedPool sp = ss_pool(S.seed[i]);
+    for (int r = 0; r < reps; r++) {
+      Pcg g = ss_child(sp, 5u * (uint32_t)r);
+      int st_t, st_d, gl_t, gl_d;
+      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+      generate_map(c, g, plan, st_t, st_d, gl_t, gl_d);
+      const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+      const int len = c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t);
+      const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+      tg += t1 - t0;
+      tc += t2 - t1;
+      chk += (uint32_t)len + plan[st_t];
+    }
+  }
+  const uint64_t wv = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0) {
+    g_stamps[(wv * 32 + 0) & ((1 << 21) - 1)] = tg;
+    g_stamps[(wv * 32 + 1) & ((1 << 21) - 1)] = tc;
+  }
+  if (chk == 0xdeadbeefu) S.err[i] = 1;  // keeps the work alive
+}
+#endif
+
 // Initial traffic of the envs k_env reset in this launch (its work list), one lane per env with
 // the reset scratch in LDS; the observation k_env wrote for them gets the new cars' squares.
 // `lanes` envs per 256-lane workgroup, lanes/4 per wave (all four SIMDs, narrower divergence).
@@ -2684,6 +2742,29 @@ int pgtg_error_count(pgtg_handle* h, uint64_t* n_errors, int32_t* first_code) {
 }
 
 #ifdef PGTG_STAMPS
+// Map generation alone: `active` lanes of every wave run `reps` generate_map + compile_path from
+// their env's seed; per-wave cycle sums (generate, compile) land in g_stamps slots 0 and 1.
+int pgtg_gen_bench(pgtg_handle* h, int32_t reps, int32_t active, float* ms) {
+  if (!h || reps < 1 || active < 1 || active > 64) return PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  const int pdw = h->L.plan_stride_dw;
+  const size_t lds = (size_t)kBlock * pdw * 4;
+  const unsigned blocks = (unsigned)((h->n + kBlock - 1) / kBlock);
+  hipEvent_t e0, e1;
+  HIPCHK(h, hipEventCreate(&e0));
+  HIPCHK(h, hipEventCreate(&e1));
+  HIPCHK(h, hipEventRecord(e0, h->stream));
+  hipLaunchKernelGGL(k_gen_bench, dim3(blocks), dim3(kBlock), lds, h->stream, h->dcfg, h->dtab, h->S, reps, active, pdw);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipEventRecord(e1, h->stream));
+  HIPCHK(h, hipEventSynchronize(e1));
+  float t = 0.f;
+  HIPCHK(h, hipEventElapsedTime(&t, e0, e1));
+  if (ms) *ms = t;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return PGTG_OK;
+}
 int pgtg_read_stamps(uint64_t* out, uint64_t n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
 }
