@@ -88,6 +88,7 @@ struct DevCfg {
   int32_t vis_pitch, vis_words; // visited bitset: ((x+2)*vis_pitch + (y+2))
   int32_t plan_stride;          // u16 per env in the global tile-plan array (multiple of 8)
   int32_t obs_bytes;            // n_channels * win * win
+  int32_t qrec_dw;              // map-queue entry words (plan_stride / 2 + 4)
   int32_t mask_words;           // ceil(win*win/32)
 };
 
@@ -148,6 +149,10 @@ struct DevState {
   uint16_t* spawners;     // [max_spawners][n] square codes x | y<<8, x-major order
   uint32_t* tr_list;      // [n] envs k_env reset this launch (k_traffic's work list)
   uint32_t* tr_count;     // [2] list lengths, alternating launches
+  // map queue (k_envq): per env a ring of kQueueDepth pre-generated episode maps, entry = plan
+  // words then {px | py<<16, sg, path_len | error<<16, 0}; qstate = count | head<<2 (0: empty)
+  uint32_t* qbuf;         // [n][kQueueDepth][qrec_dw] or null
+  uint8_t* qstate;        // [n] or null
   uint8_t* err;           // [n] last error code (negated PGTG_E_*)
   unsigned long long* counters;  // [2]: env steps, episodes
   const int8_t* nsd_tab;

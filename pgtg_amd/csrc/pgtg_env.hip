@@ -1374,16 +1374,17 @@ __device__ __forceinline__ uint32_t udiv_f(uint32_t x, uint32_t d, float inv) {
   return q;
 }
 
-// Threads [t0, t0 + nthr) of the workgroup share the chunks (all of them, or helper waves).
+// `nthr` threads share the chunks, this one with rank `rank` (default: the whole workgroup).
 __device__ __forceinline__ void write_obs(uint8_t* __restrict__ dst, uint32_t cnt, uint32_t WW, uint32_t MW,
-                                          uint32_t C, const uint32_t* st, const uint8_t* sel, int t0 = 0,
+                                          uint32_t C, const uint32_t* st, const uint8_t* sel, int rank = -1,
                                           int nthr = kBlock) {
+  if (rank < 0) rank = (int)threadIdx.x;
   const uint32_t OB = C * WW, total = cnt * OB;
   const uintptr_t a0 = (uintptr_t)dst;
   const uintptr_t c0 = a0 & ~(uintptr_t)15;
   const uint32_t nchunks = (uint32_t)((a0 + total - c0 + 15) >> 4);
   const float invWW = 1.0f / (float)WW, invOB = 1.0f / (float)OB;
-  for (uint32_t ch = (uint32_t)((int)threadIdx.x - t0); ch < nchunks; ch += (uint32_t)nthr) {
+  for (uint32_t ch = (uint32_t)rank; ch < nchunks; ch += (uint32_t)nthr) {
     const int r = (int)((intptr_t)(c0 + ((uintptr_t)ch << 4)) - (intptr_t)a0);  // > -16
     const uint32_t lo = r < 0 ? 0u : (uint32_t)r;
     const uint32_t hi = min((uint32_t)(r + 15), total - 1u);
@@ -1434,7 +1435,11 @@ struct Lds {
   int stream_words;    // observation image words (+2 pad)
   int spread;          // env slots spread over the four waves (traffic: long per-lane chains)
   int compact;         // resets run on dense lanes (wave 0 first) instead of on their env's lane
+  int queue;           // step launches use k_envq (maps generated one episode ahead by helper waves)
+  int gen_off;         // k_envq: word offset of the helper lanes' plan scratch (kQueueLanes x plan_stride_dw)
 };
+constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
+constexpr int kQueueDepth = 3;   // queued maps per env (a ring)
 
 __host__ __device__ inline int odd_up(int x) { return x | 1; }
 
@@ -1454,11 +1459,17 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);  // tuning knob
   l.compact = 1;
   if (const char* e = getenv("PGTG_COMPACT")) l.compact = atoi(e);  // tuning knob
+  // map queue: random maps without traffic, a whole-workgroup observation image and at least one
+  // wave without env slots
+  l.queue = !c.need_car && !c.fixed_map && envs <= kBlock - 64 && l.sub_envs >= envs;
+  if (const char* e = getenv("PGTG_QUEUE")) l.queue = l.queue && atoi(e);  // tuning knob
+  l.gen_off = (int)(((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
+                    (kBlock + 128) / 4);
   return l;
 }
 __host__ inline size_t lds_bytes(const Lds& l) {
   return (size_t)4 * ((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
-         kBlock + 32;
+         kBlock + 128 + (l.queue ? (size_t)4 * kQueueLanes * l.plan_stride_dw : 0);
 }
 
 enum { MODE_STEP = 0, MODE_RESET_SEEDED = 1, MODE_RESET_UNSEEDED = 2, MODE_OBSERVE = 3 };
@@ -1663,7 +1674,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (tid == 0 && n_resets) atomicAdd(&S.counters[1], (unsigned long long)n_resets);
   if (helpers && want_final && out.final_obs && tid >= t_help)
     write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
-              (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel, t_help, kBlock - t_help);
+              (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel, tid - t_help, kBlock - t_help);
   if (L.compact) {
     if (wslot >= 0) {
       uint32_t* xw = lds + xf_off + wslot * xf_dw;
@@ -1721,6 +1732,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       if ((TR && c.need_car)) S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.bank, 0u);
     }
     if (mode != MODE_OBSERVE || err) S.err[i] = (uint8_t)(-err);
+    if (S.qstate && reset_now) S.qstate[i] = 0;  // maps generated here: the queued ones are stale
   }
   if (TR && c.need_car) {
     // k_traffic's work list: one wave-aggregated atomic per wave
@@ -1752,6 +1764,269 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
                  slot);
   }
   if (mode == MODE_STEP && tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
+  STAMP(6);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Map queue.  Everything env_reset derives from the map stream -- the map, its compiled path, the
+// start square -- depends only on (seed, spawn counter), not on the episode before it, so the next
+// two episodes' maps of every env are generated ahead and a reset takes the head of the env's ring.
+// ------------------------------------------------------------------------------------------------
+// One ring entry: generate_map + compile_path + the start draw of env_reset for spawn counter `k`,
+// built in the lane's LDS plan scratch and written to HBM.
+__device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState& S, uint64_t i, uint32_t k,
+                                                uint16_t* plan, int pdw, uint32_t* __restrict__ dst) {
+  SeedPool sp = ss_pool(S.seed[i]);
+  Pcg map_rng = ss_child(sp, k);
+  int st_t, st_d, gl_t, gl_d;
+  generate_map(c, map_rng, plan, st_t, st_d, gl_t, gl_d);
+  const int len = c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t);
+  int px = 0, py = 0, err = 0;
+  if (len == 0 || !((plan_exits(plan[st_t]) >> st_d) & 1u)) {
+    err = PGTG_E_MAP;
+  } else {  // env_reset's starter square (pgtg/map.py:31-34)
+    const int j = (int)pcg_int(map_rng, 3);
+    const int tx = st_t % c.tw, ty = st_t / c.tw;
+    int lx, ly;
+    switch (st_d) {
+      case 0: lx = 3 + j; ly = 0; break;
+      case 1: lx = 8; ly = 3 + j; break;
+      case 2: lx = 3 + j; ly = 8; break;
+      default: lx = 0; ly = 3 + j; break;
+    }
+    px = tx * kTile + lx;
+    py = ty * kTile + ly;
+  }
+  const uint32_t* pw = reinterpret_cast<const uint32_t*>(plan);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  const int pwords = c.plan_stride / 2;
+  for (int q = 0; q < pwords / 4; q++) {
+    uint32_t wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) wv[j] = (q * 4 + j < pdw) ? pw[q * 4 + j] : 0u;
+    d4[q] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+  }
+  d4[pwords / 4] = make_uint4(((uint32_t)px & 0xffffu) | ((uint32_t)py << 16),
+                              (uint32_t)st_t | (uint32_t)st_d << 8 | (uint32_t)gl_t << 16 | (uint32_t)gl_d << 24,
+                              (uint32_t)len | (uint32_t)(-err) << 16, 0u);
+}
+
+// Barrier among the waves of a workgroup that take part (lane 0 of each arrives at an LDS counter
+// that only grows; `target` = uses so far x participating waves), for phases that must not wait
+// for a wave busy elsewhere.
+__device__ __forceinline__ void sub_barrier(uint32_t* ctr, uint32_t target) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Step launch with the map queue (no traffic; workgroups of <= 192 envs).  Wave `env_waves` (the
+// first without env slots) refills the rings of the envs that took a map in earlier launches --
+// at most kQueueLanes entries per launch, empty rings' heads first -- while the other waves step,
+// write the terminal observations, take queued maps for the envs that finished and write the new
+// observations, synchronising among themselves only.  Only when some env's ring is empty (the
+// first step after a reset, or a refill carried over) do they wait for the head refills.
+__global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
+                                                    DevState S, const uint8_t* __restrict__ actions, PgtgOutputs out,
+                                                    Lds L) {
+  extern __shared__ uint32_t lds[];
+  const DevCfg& c = *cfg;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  STAMP(0);
+  {
+    const int words = (int)((c.generic_channels ? sizeof(Tables) : offsetof(Tables, lanes)) / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
+    uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
+    for (int k = tid; k < words; k += blockDim.x) dstt[k] = src[k];
+  }
+  const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
+  const int nb = (int)min((uint64_t)L.envs, S.n - env0);
+  const int env_waves = (L.envs + 63) / 64, gen_wave = env_waves;
+  const bool env_wave = wave < env_waves;
+  const int slot = tid;
+  const uint64_t i = env0 + slot;
+  const bool live = env_wave && slot < nb;
+  const int pdw = L.plan_stride_dw;
+  uint32_t* plan_w = lds + (env_wave ? slot : 0) * pdw;
+  uint32_t* xf = lds + L.envs * pdw;  // per env slot: spawn counter, ring state at launch start
+  uint32_t* st = lds + L.envs * (pdw + L.scratch_dw + L.traf_dw + L.hist_dw);
+  uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
+  uint64_t* fm = reinterpret_cast<uint64_t*>(sel + kBlock);  // [level][env wave]: envs refilled at ring level
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(fm + 3 * kQueueDepth);  // sub_barrier counter
+  Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
+
+  EnvView v{};
+  uint32_t qs = 0;
+  if (live) {
+    v = rec_load(S.rec, i);
+    qs = S.qstate[i];
+    const uint4* src = reinterpret_cast<const uint4*>(S.plan + i * (uint64_t)c.plan_stride);
+    for (int k = 0; k < c.plan_stride / 8; k++) {
+      uint4 w4 = src[k];
+      uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (k * 4 + j < pdw) plan_w[k * 4 + j] = wv[j];
+    }
+    xf[slot * L.scratch_dw] = v.spawn;
+    xf[slot * L.scratch_dw + 1] = qs;
+  }
+  const uint32_t qn = qs & 3u, qh = (qs >> 2) & 3u;
+  if (env_wave) {  // refills: ring level l (0 = head) for the envs holding <= l maps
+#pragma unroll
+    for (int l = 0; l < kQueueDepth; l++) {
+      const uint64_t m = __ballot(live && qn <= (uint32_t)l);
+      if (lane == 0) fm[l * 3 + wave] = m;
+    }
+  }
+  if (tid == 0) *ctr = 0u;
+  __syncthreads();  // tables, plans, refill masks, counter
+  STAMP(1);
+  // refills: the heads of empty rings (level 0, all of them), then levels 1.. in order (the first
+  // kQueueLanes this launch; the rest wait for a later launch)
+  int F[kQueueDepth];
+#pragma unroll
+  for (int l = 0; l < kQueueDepth; l++) {
+    F[l] = 0;
+    for (int w = 0; w < env_waves; w++) F[l] += __popcll(fm[l * 3 + w]);
+  }
+  const bool any_empty = F[0] != 0;
+
+  if (wave == gen_wave) {
+    uint16_t* gplan = reinterpret_cast<uint16_t*>(lds + L.gen_off + lane * pdw);
+    auto refill = [&](int k, int l) {
+      int e = 0, pre = 0;
+      for (int w = 0; w < env_waves; w++) {
+        const uint64_t m = fm[l * 3 + w];
+        const int cw = __popcll(m);
+        if (k >= pre && k < pre + cw) e = w * 64 + select64(m, k - pre);
+        pre += cw;
+      }
+      const uint64_t ie = env0 + e;
+      const uint32_t qe = xf[e * L.scratch_dw + 1];
+      const uint32_t rslot = (((qe >> 2) & 3u) + (uint32_t)l) % (uint32_t)kQueueDepth;
+      gen_queue_entry(c, S, ie, xf[e * L.scratch_dw] + 5u * (uint32_t)l, gplan, pdw,
+                      S.qbuf + (ie * kQueueDepth + rslot) * (uint64_t)c.qrec_dw);
+    };
+    for (int k = lane; k < F[0]; k += kQueueLanes) refill(k, 0);  // every empty ring's head
+    if (any_empty) __syncthreads();  // head refills visible to the other waves
+    {
+      int k = lane, l = 1;
+      while (l < kQueueDepth && k >= F[l]) {
+        k -= F[l];
+        l++;
+      }
+      if (l < kQueueDepth) refill(k, l);
+    }
+    STAMP(7);
+    return;
+  }
+
+  // ---- env and writer waves (all but the refill wave) ----
+  const int np = kBlock / 64 - 1;                            // participating waves
+  const int rank = (wave < gen_wave ? wave : wave - 1) * 64 + lane, nthr = np * 64;
+  uint8_t my_sel = 0;
+  int err = 0;
+  if (live) {
+    StepResult res{0.0, 0.0, 0u};
+    bool occ_sat = false;
+    TrafState ts{0, 0, 0, 0};
+    err = env_step<false>(c, S, i, v, pl, actions[i], res, nullptr, occ_sat, nullptr, ts, nullptr);
+    const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
+    if (out.reward) out.reward[i] = res.reward;
+    if (out.cost) out.cost[i] = res.cost;
+    if (out.terminated) out.terminated[i] = (v.flags & kFlagTerminated) ? 1 : 0;
+    if (out.truncated) out.truncated[i] = (v.flags & kFlagTruncated) ? 1 : 0;
+    if (out.braking) out.braking[i] = 0;
+    my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
+    ObsInfo oi;  // the post-step image of every env (terminal for the finished ones)
+    build_obs<false>(c, S, pl, v, st + slot * L.seg_words, oi, nullptr);
+    write_small_outputs(c, out, i, v, oi, my_sel == 1);
+  }
+  if (env_wave) sel[slot] = my_sel;
+  const uint64_t rm = __ballot(my_sel == 1);
+  if (env_wave && lane == 0 && rm) atomicAdd(&S.counters[1], (unsigned long long)__popcll(rm));
+  STAMP(2);
+  sub_barrier(ctr, (uint32_t)np);
+  if (out.final_obs)
+    write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
+              (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel, rank, nthr);
+  STAMP(3);
+  sub_barrier(ctr, 2u * np);  // terminal images written before they are rebuilt
+  if (any_empty) __syncthreads();  // the head refills
+  const bool reset_now = my_sel != 0;
+  if (reset_now) {  // the ring's head becomes the episode (env_reset without the generation)
+    const uint4* q4 = reinterpret_cast<const uint4*>(S.qbuf + (i * kQueueDepth + qh) * (uint64_t)c.qrec_dw);
+    uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
+    const int pwords = c.plan_stride / 2;
+    for (int k = 0; k < pwords / 4; k++) {
+      const uint4 w4 = q4[k];
+      dstp[k] = w4;
+      const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (k * 4 + j < pdw) plan_w[k * 4 + j] = wv[j];
+    }
+    const uint4 meta = q4[pwords / 4];
+    const uint32_t k0 = v.spawn;
+    if (c.need_ice || c.need_broken || c.need_sand) {
+      SeedPool sp = ss_pool(S.seed[i]);
+      if (c.need_ice) stream_store_all(S.ice, i, ss_child(sp, k0 + 2u));
+      if (c.need_broken) stream_store_all(S.broken, i, ss_child(sp, k0 + 3u));
+      if (c.need_sand) stream_store_all(S.sand, i, ss_child(sp, k0 + 4u));
+    }
+    v.spawn = k0 + 5u;
+    v.sg = meta.y;
+    v.used = 0;
+    v.path_len = meta.z & 0xffffu;
+    v.flags = 0;
+    v.phase = 0;
+    v.elapsed = 0;
+    v.vx = v.vy = 0;
+    v.px = (int)(int16_t)(meta.x & 0xffffu);
+    v.py = (int)(int16_t)(meta.x >> 16);
+    const int e2 = -(int)(meta.z >> 16);
+    if (e2) err = e2;
+    if (S.visited && e2 == 0) {
+      uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
+      for (int q2 = 0; q2 < c.vis_words; q2++) vis[q2] = 0;
+      int b = (v.px + 2) * c.vis_pitch + (v.py + 2);
+      vis[b >> 5] |= 1u << (b & 31);
+    }
+  }
+  STAMP(4);
+  if (live) {
+    rec_store(S.rec, i, v);
+    S.err[i] = (uint8_t)(-err);
+    // ring entries after this launch: the refills served (same list order as the refill wave)
+    // minus the head a reset took
+    uint32_t have = qn == 0u ? 1u : qn;
+    int base = 0;  // list index of the first item of the level
+#pragma unroll
+    for (int l = 1; l < kQueueDepth; l++) {
+      int pre = 0;
+      for (int w = 0; w < wave; w++) pre += __popcll(fm[l * 3 + w]);
+      if (qn <= (uint32_t)l && base + pre + __popcll(fm[l * 3 + wave] & ((1ull << lane) - 1ull)) < kQueueLanes) have++;
+      base += F[l];
+    }
+    const uint32_t nq = reset_now ? have - 1u : have;  // have >= 1: every head is refilled
+    const uint32_t nh = reset_now ? (qh + 1u) % (uint32_t)kQueueDepth : qh;
+    S.qstate[i] = (uint8_t)(nq | nh << 2);
+  }
+  STAMP(5);
+  if (reset_now) {
+    ObsInfo oi;
+    build_obs<false>(c, S, pl, v, st + slot * L.seg_words, oi, nullptr);
+    write_small_outputs(c, out, i, v, oi, false);
+  }
+  STAMP(30);
+  sub_barrier(ctr, 3u * np);
+  STAMP(31);
+  if (out.obs)
+    write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
+              (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, nullptr, rank, nthr);
+  if (tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
   STAMP(6);
 }
 
@@ -2224,6 +2499,7 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
   c.vis_pitch = c.H + 4;
   c.vis_words = ((c.W + 4) * (c.H + 4) + 31) / 32;
   c.plan_stride = ((c.nt + 7) / 8) * 8;
+  c.qrec_dw = c.plan_stride / 2 + 4;
   return 0;
 }
 
@@ -2426,6 +2702,18 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
         (void)hipFuncSetAttribute((const void*)k_traffic, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->kt_lds);
     }
   }
+  // map queue (k_envq): recheck after the adjustments above, place the helper scratch, allocate
+  h->L.queue = h->L.queue && h->L.sub_envs >= h->L.envs && h->L.envs <= kBlock - 64;
+  h->L.gen_off = (int)(((size_t)h->L.envs * (h->L.plan_stride_dw + h->L.scratch_dw + h->L.traf_dw + h->L.hist_dw) +
+                        h->L.stream_words) + (kBlock + 128) / 4);
+  if (h->L.queue && lds_bytes(h->L) + sizeof(Tables) > 40 * 1024) h->L.queue = 0;  // keep 4 workgroups per CU
+  if (h->L.queue) {
+    if ((rc = dalloc(h, &h->S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw)) || (rc = dalloc(h, &h->S.qstate, n))) {
+      g_create_err = h->err;
+      pgtg_destroy(h);
+      return rc;
+    }
+  }
   h->lds = lds_bytes(h->L);
   if (h->lds + sizeof(Tables) > 160 * 1024) {
     g_create_err = "LDS budget exceeded";
@@ -2436,6 +2724,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
   {
     (void)hipFuncSetAttribute((const void*)k_env<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
     (void)hipFuncSetAttribute((const void*)k_env<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+    (void)hipFuncSetAttribute((const void*)k_envq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
   }
   *out = h;
   return PGTG_OK;
@@ -2479,6 +2768,9 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
   if (h->hcfg.need_car || h->hcfg.n_rules > 0)
     hipLaunchKernelGGL(k_env<true>, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
                        actions, mask, h->out, mode, h->L, h->tr_slot);
+  else if (mode == MODE_STEP && h->L.queue)
+    hipLaunchKernelGGL(k_envq, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
+                       actions, h->out, h->L);
   else
     hipLaunchKernelGGL(k_env<false>, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
                        actions, mask, h->out, mode, h->L, h->tr_slot);

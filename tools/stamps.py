@@ -33,7 +33,7 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
     env = PGTGVecEnv(N, device=0, **kw)
     E, lds = env.launch_info()
     env.reset(seed=0)
-    for k in range(30):
+    for k in range(int(os.environ.get("PGTG_STAMP_STEPS", "30"))):
         env.step_random(1, k)
     torch.cuda.synchronize()
     blocks = (N + E - 1) // E
@@ -45,6 +45,14 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
     # traffic workgroups spread their env slots over all four waves; otherwise envs fill waves in order
     spread = kw.get("traffic_density", 0) > 0
     active = np.ones(nw, bool) if spread else (np.arange(nw) % 4) * 64 < E
+    helper = (np.arange(nw) % 4) * 64 == ((E + 63) // 64) * 64
+    sh = st[helper]
+    okh = (sh[:, 7] > sh[:, 0]) & (sh[:, 7] - sh[:, 0] < 1e8)
+    if okh.any():  # map-queue helper wave (k_envq)
+        print(f"  queue helper wave: fills {int((sh[okh, 7] - sh[okh, 1]).mean())} cycles "
+              f"(max {int((sh[okh, 7] - sh[okh, 1]).max())}), start {int((sh[okh, 1] - sh[okh, 0]).mean())}; "
+              f"generate {int((sh[okh, 10] - sh[okh, 9]).mean()) if False else int((sh[okh, 15] - sh[okh, 14]).mean())} "
+              f"(removal, last fill)", flush=True)
     st = st[active]
     d = np.diff(st[:, :7], axis=1)
     print(f"{name}: {N} envs, {E} envs/workgroup, LDS {lds} B; cycles per active wave (last launch)", flush=True)
