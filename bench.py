@@ -177,7 +177,8 @@ def main():
                          "frac": achieved / PEAK_HBM_GBS, "traffic": load_traffic(args.workload, alg),
                          "kernel": "pgtg::k_env (step + auto-reset)", "avg_kernel_us": avg_kernel_s * 1e6,
                          "alg_bytes_per_launch": alg, "resets_per_launch": resets_per_launch,
-                         "envs_per_workgroup": env.launch_info()[0], "lds_bytes": env.launch_info()[1]},
+                         "envs_per_workgroup": env.launch_info()[0], "lds_bytes": env.launch_info()[1],
+                         "workgroups_per_cu": env.occupancy()},
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)

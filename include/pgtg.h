@@ -193,6 +193,8 @@ int pgtg_window(const pgtg_handle* h);
 uint64_t pgtg_num_envs(const pgtg_handle* h);
 /* Launch geometry of the step kernel: envs per 256-lane workgroup and dynamic LDS bytes. */
 int pgtg_launch_info(const pgtg_handle* h, int32_t* envs_per_block, int32_t* lds_bytes);
+/* Resident workgroups per CU of the step kernel this handle launches (HIP occupancy query). */
+int pgtg_occupancy(const pgtg_handle* h, int32_t* step_blocks_per_cu);
 const char* pgtg_last_error(const pgtg_handle* h);
 /* Per-launch device timing of the step kernels with HIP events on the handle's stream.  every > 0:
  * every every-th pgtg_step brackets its kernels with an event pair (1: all; 0: off);

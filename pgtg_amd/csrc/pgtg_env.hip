@@ -1469,7 +1469,7 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
 }
 __host__ inline size_t lds_bytes(const Lds& l) {
   return (size_t)4 * ((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
-         kBlock + 128 + (l.queue ? (size_t)4 * kQueueLanes * l.plan_stride_dw : 0);
+         kBlock + (l.queue ? 128 + (size_t)4 * kQueueLanes * l.plan_stride_dw : 32);
 }
 
 enum { MODE_STEP = 0, MODE_RESET_SEEDED = 1, MODE_RESET_UNSEEDED = 2, MODE_OBSERVE = 3 };
@@ -3064,6 +3064,15 @@ int pgtg_read_stamps(uint64_t* out, uint64_t n) {
 
 int pgtg_window(const pgtg_handle* h) { return h ? h->hcfg.win : 0; }
 uint64_t pgtg_num_envs(const pgtg_handle* h) { return h ? h->n : 0; }
+int pgtg_occupancy(const pgtg_handle* h, int32_t* step_blocks_per_cu) {
+  if (!h) return PGTG_E_INVALID;
+  int nb = 0;
+  const void* fn = h->L.queue ? (const void*)k_envq : (h->hcfg.need_car ? (const void*)k_env<true> : (const void*)k_env<false>);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kBlock, h->lds) != hipSuccess) return PGTG_E_DEVICE;
+  if (step_blocks_per_cu) *step_blocks_per_cu = nb;
+  return PGTG_OK;
+}
+
 int pgtg_launch_info(const pgtg_handle* h, int32_t* envs_per_block, int32_t* lds_bytes) {
   if (!h) return PGTG_E_INVALID;
   if (envs_per_block) *envs_per_block = h->L.envs;

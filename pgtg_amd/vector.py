@@ -279,6 +279,12 @@ class PGTGVecEnv:
         _check(self._lib.pgtg_launch_info(self._h, C.byref(e), C.byref(b)), self._h)
         return e.value, b.value
 
+    def occupancy(self) -> int:
+        """Workgroups of the step kernel resident per CU (HIP occupancy query)."""
+        n = C.c_int32()
+        _check(self._lib.pgtg_occupancy(self._h, C.byref(n)), self._h)
+        return n.value
+
     def counters(self) -> tuple[int, int]:
         a, b = C.c_uint64(), C.c_uint64()
         _check(self._lib.pgtg_get_counters(self._h, C.byref(a), C.byref(b)), self._h)

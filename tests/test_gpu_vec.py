@@ -128,3 +128,19 @@ def test_sharded_batch_equals_the_global_batch():
             assert torch.equal(full.reward[r * n:(r + 1) * n], h.reward), (t, r)
     for i in (0, n - 1, n, 2 * n - 1):
         assert np.array_equal(full.cars(i), halves[i // n].cars(i % n))
+
+
+@pytest.mark.parametrize("n,kw,want", [
+    (65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5), 2),  # configs[2]
+    (131072, dict(random_map_width=5, random_map_height=5), 4),                       # configs[4] shard
+    (262144, dict(random_map_width=3, random_map_height=3), 4),                       # configs[3]
+])
+def test_step_kernel_occupancy(n, kw, want):
+    """The LDS sizing of the bench workloads keeps the intended workgroups per CU resident (a few
+    bytes over the budget once halved cfg3's throughput: one traffic workgroup per CU)."""
+    from pgtg_amd.vector import PGTGVecEnv
+    vec = PGTGVecEnv(n, spec=_spec(**kw))
+    try:
+        assert vec.occupancy() >= want, (vec.launch_info(), vec.occupancy())
+    finally:
+        vec.close()
