@@ -820,15 +820,53 @@ __device__ __forceinline__ bool nearest_goal_square(const DevCfg& c, const Plan&
   return found;
 }
 
-// Observation of one env into its LDS segments: channel ci occupies words seg[ci*MW .. +MW) with
-// bit b = window square b (row-major over x, then y), unused high bits zero.  Plain stores only.
+// The observation image in LDS is a dense bit stream in output byte order: bit k = byte k of the
+// image's slice of the uint8 output (env slot e, channel ci, window square b at bit
+// e*C*WW + ci*WW + b).  A writer then turns any 16 consecutive bits into one 16-byte store with a
+// funnel shift, whatever the window size.  An env's first and last words are shared with its
+// neighbours in the stream and are merged with LDS and/or atomics (the neighbours' bits are
+// disjoint, so concurrent merges commute); the words in between are plain stores.
+struct BitSink {
+  uint32_t* st;
+  uint32_t w, fill, own;  // current word, bits held, bits of the current word this env owns
+  uint64_t acc;
+  __device__ __forceinline__ BitSink(uint32_t* s, uint32_t bit0)
+      : st(s), w(bit0 >> 5), fill(bit0 & 31u), own(~0u << (bit0 & 31u)), acc(0) {}
+  __device__ __forceinline__ void emit(uint32_t val, uint32_t mask) {
+    if (mask == ~0u) {
+      st[w] = val;
+    } else {
+      __hip_atomic_fetch_and(st + w, ~mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_or(st + w, val & mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  // append the n (1..32) low bits of val (higher bits zero)
+  __device__ __forceinline__ void put(uint32_t val, uint32_t n) {
+    acc |= (uint64_t)val << fill;
+    fill += n;
+    if (fill >= 32u) {
+      emit((uint32_t)acc, own);
+      own = ~0u;
+      acc >>= 32;
+      fill -= 32u;
+      w++;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    if (fill) emit((uint32_t)acc, own & ((1u << fill) - 1u));
+  }
+};
+
+// Observation of one env into the image at bit offset bit0 (see BitSink): channel by channel, each
+// the window's squares row-major over x, then y.
 template <bool TR>
 __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
-                                          uint32_t* seg, ObsInfo& oi, const uint8_t* occ) {
+                                          uint32_t* img, uint32_t bit0, ObsInfo& oi, const uint8_t* occ) {
+  BitSink sink(img, bit0);
   int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
   int tx = pix / kTile, ty = piy / kTile;
   int color = phase_color(c, v.phase);
-  const int WW = c.win * c.win, MW = c.mask_words;
+  const int WW = c.win * c.win;
   if (!c.sliding) {
     oi.x0 = tx * kTile;
     oi.y0 = ty * kTile;
@@ -897,9 +935,9 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
         }
         out3[k] = val;
       }
-      seg[ci * 3 + 0] = out3[0];
-      seg[ci * 3 + 1] = out3[1];
-      seg[ci * 3 + 2] = out3[2] & 0x1ffffu;  // 81 = 32 + 32 + 17 bits
+      sink.put(out3[0], 32u);
+      sink.put(out3[1], 32u);
+      sink.put(out3[2] & 0x1ffffu, 17u);  // 81 = 32 + 32 + 17 bits
     }
   } else {
     const int win = c.win;
@@ -933,10 +971,11 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
             acc |= chan_bit(code, f, lanes, sp, color) << b;
           }
         }
-        seg[ci * MW + (w0 >> 5)] = acc;
+        sink.put(acc, (uint32_t)min(32, WW - w0));
       }
     }
   }
+  sink.finish();
   oi.nsd = -1;
   if (c.next_subgoal) {
     int t = ty * c.tw + tx;
@@ -1374,48 +1413,59 @@ __device__ __forceinline__ uint32_t udiv_f(uint32_t x, uint32_t d, float inv) {
   return q;
 }
 
-// `nthr` threads share the chunks, this one with rank `rank` (default: the whole workgroup).
-__device__ __forceinline__ void write_obs(uint8_t* __restrict__ dst, uint32_t cnt, uint32_t WW, uint32_t MW,
-                                          uint32_t C, const uint32_t* st, const uint8_t* sel, int rank = -1,
-                                          int nthr = kBlock) {
+// Write `cnt` envs' observations (OB bytes each) from the dense image to dst as 16-byte stores
+// aligned to 16 B (the first and last chunks may be partial).  `nthr` threads share the chunks,
+// this one with rank `rank` (default: the whole workgroup).  With `sel`, only 128-byte lines
+// holding an env with sel == 1 are written (whole lines: the other envs' bytes in them get their
+// own image, which the API leaves unspecified, and the memory system sees no partial lines); `lm`,
+// when given, is the line mask of the selection (mark_lines) and replaces the per-env test.
+// Line mask for the selection: the 128-byte lines (counted from the one holding dst) that env e's
+// OB output bytes touch, or-ed into lm (cleared beforehand).
+__device__ __forceinline__ void mark_lines(uint32_t* lm, const uint8_t* dst, uint32_t e, uint32_t OB) {
+  const uintptr_t a0 = (uintptr_t)dst, base = a0 >> 7;
+  uint32_t l = (uint32_t)(((a0 + (uintptr_t)e * OB) >> 7) - base);
+  const uint32_t l1 = (uint32_t)(((a0 + (uintptr_t)(e + 1) * OB - 1) >> 7) - base);
+  while (l <= l1) {
+    const uint32_t hi = min(l1, l | 31u), n = hi - l + 1u;
+    __hip_atomic_fetch_or(lm + (l >> 5), (n == 32u ? ~0u : ((1u << n) - 1u)) << (l & 31u), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+    l = hi + 1u;
+  }
+}
+
+__device__ __forceinline__ void write_obs(uint8_t* __restrict__ dst, uint32_t cnt, uint32_t OB, const uint32_t* st,
+                                          const uint8_t* sel, int rank = -1, int nthr = kBlock,
+                                          const uint32_t* lm = nullptr) {
   if (rank < 0) rank = (int)threadIdx.x;
-  const uint32_t OB = C * WW, total = cnt * OB;
+  const uint32_t total = cnt * OB;
   const uintptr_t a0 = (uintptr_t)dst;
   const uintptr_t c0 = a0 & ~(uintptr_t)15;
   const uint32_t nchunks = (uint32_t)((a0 + total - c0 + 15) >> 4);
-  const float invWW = 1.0f / (float)WW, invOB = 1.0f / (float)OB;
+  const float invOB = 1.0f / (float)OB;
   for (uint32_t ch = (uint32_t)rank; ch < nchunks; ch += (uint32_t)nthr) {
     const int r = (int)((intptr_t)(c0 + ((uintptr_t)ch << 4)) - (intptr_t)a0);  // > -16
-    const uint32_t lo = r < 0 ? 0u : (uint32_t)r;
-    const uint32_t hi = min((uint32_t)(r + 15), total - 1u);
-    if (sel) {
-      const uint32_t e0 = udiv_f(lo, OB, invOB), e1 = udiv_f(hi, OB, invOB);
+    if (lm) {
+      const uint32_t li = (uint32_t)(((c0 + ((uintptr_t)ch << 4)) >> 7) - (a0 >> 7));
+      if (!((lm[li >> 5] >> (li & 31u)) & 1u)) continue;
+    } else if (sel) {
+      const intptr_t l0 = (intptr_t)((c0 + ((uintptr_t)ch << 4)) & ~(uintptr_t)127) - (intptr_t)a0;
+      const uint32_t llo = l0 < 0 ? 0u : (uint32_t)l0;
+      const uint32_t lhi = min((uint32_t)(l0 + 127), total - 1u);
+      const uint32_t e0 = udiv_f(llo, OB, invOB), e1 = udiv_f(lhi, OB, invOB);
       bool any = false;
       for (uint32_t e = e0; e <= e1; e++) any = any || sel[e] == 1;
       if (!any) continue;
     }
-    // gather bits lo..hi from the segment image
-    uint32_t g = udiv_f(lo, WW, invWW), sq = lo - g * WW;
-    uint32_t bits = 0;
-    int got = (int)lo - r;  // bit index inside the chunk of byte `lo`
-    const int need = (int)hi - r + 1;
-    while (got < need) {
-      uint32_t take = min((uint32_t)(need - got), WW - sq);
-      uint32_t wi = g * MW + (sq >> 5), sh = sq & 31u;
-      uint64_t two = (uint64_t)st[wi] | ((uint64_t)st[wi + 1] << 32);
-      uint32_t part = (uint32_t)(two >> sh) & ((1u << take) - 1u);
-      bits |= part << got;
-      got += (int)take;
-      g++;
-      sq = 0;
-    }
     uint8_t* cp = dst + r;  // 16-byte aligned
     if (r >= 0 && (uint32_t)r + 16u <= total) {
+      const uint32_t w = (uint32_t)r >> 5;
+      const uint64_t two = (uint64_t)st[w] | ((uint64_t)st[w + 1] << 32);
+      const uint32_t bits = (uint32_t)(two >> (r & 31));
       *reinterpret_cast<uint4*>(cp) = make_uint4(expand4(bits), expand4(bits >> 4), expand4(bits >> 8), expand4(bits >> 12));
     } else {
       for (int b = 0; b < 16; b++) {
-        int rb = r + b;
-        if (rb >= 0 && (uint32_t)rb < total) cp[b] = (uint8_t)((bits >> b) & 1u);
+        const int rb = r + b;
+        if (rb >= 0 && (uint32_t)rb < total) cp[b] = (uint8_t)((st[rb >> 5] >> (rb & 31)) & 1u);
       }
     }
   }
@@ -1430,19 +1480,25 @@ struct Lds {
   int scratch_dw;      // per-env reset hand-over words (odd): spawn in; position, sg, path length out
   int traf_dw;         // per-lane traffic region words (occupancy counters / reset scratch), odd or 0
   int hist_dw;         // per-lane route histogram words for the braking rules, odd or 0
-  int seg_words;       // per-env observation words (n_channels * mask_words)
+  int seg_bits;        // per-env observation bits in the dense image (= output bytes per env)
   int sub_envs;        // envs per observation sub-batch (== envs when they all fit)
-  int stream_words;    // observation image words (+2 pad)
+  int stream_words;    // observation image words (dense bit stream of sub_envs envs, +2 pad)
   int spread;          // env slots spread over the four waves (traffic: long per-lane chains)
   int compact;         // resets run on dense lanes (wave 0 first) instead of on their env's lane
   int queue;           // step launches use k_envq (maps generated one episode ahead by helper waves)
   int gen_off;         // k_envq: word offset of the helper lanes' plan scratch (kQueueLanes x plan_stride_dw)
+  int lm_words;        // terminal-observation line mask words (0: test the selection bytes)
+  int diag;            // diagnostic experiments (PGTG_DIAG; 0 in normal runs)
 };
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
 constexpr int kQueueDepth = 3;   // queued maps per env (a ring)
 
 __host__ __device__ inline int odd_up(int x) { return x | 1; }
+// words of a dense observation image of `envs` envs (+2: the writers' funnel reads run one word
+// ahead; a multiple of 4 so that what follows stays 16-byte aligned)
+__host__ inline int img_words(int envs, int bits) { return ((int)(((int64_t)envs * bits + 31) / 32) + 2 + 3) & ~3; }
 
+__host__ inline void lds_tail(Lds& l, const DevCfg& c);
 __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   Lds l;
   l.envs = envs;
@@ -1450,11 +1506,11 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.scratch_dw = c.need_car ? 0 : 3;  // with traffic: inside the (by then dead) occupancy counters
   l.traf_dw = c.need_car ? odd_up(c.traf_bytes / 4) : 0;
   l.hist_dw = c.n_rules > 0 ? 5 : 0;
-  l.seg_words = c.n_channels * c.mask_words;
+  l.seg_bits = c.n_channels * c.win * c.win;
   const int budget_words = 12 * 1024;  // 48 KiB observation image
-  int sub = l.seg_words > 0 ? (budget_words - 2) / l.seg_words : envs;
+  int sub = l.seg_bits > 0 ? (int)(((int64_t)budget_words - 3) * 32 / l.seg_bits) : envs;
   l.sub_envs = sub > envs ? envs : (sub < 1 ? 1 : sub);
-  l.stream_words = l.sub_envs * l.seg_words + 2;
+  l.stream_words = img_words(l.sub_envs, l.seg_bits);
   l.spread = c.need_car ? 1 : 0;
   if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);  // tuning knob
   l.compact = 1;
@@ -1463,13 +1519,28 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   // wave without env slots
   l.queue = !c.need_car && !c.fixed_map && envs <= kBlock - 64 && l.sub_envs >= envs;
   if (const char* e = getenv("PGTG_QUEUE")) l.queue = l.queue && atoi(e);  // tuning knob
-  l.gen_off = (int)(((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
-                    (kBlock + 128) / 4);
+  l.diag = 0;
+  if (const char* e = getenv("PGTG_DIAG")) l.diag = atoi(e);  // diagnostic experiments only
+  lds_tail(l, c);
   return l;
+}
+// After the observation image: sel[kBlock] | 32 B (k_env: per-wave reset ballots) or 128 B (k_envq:
+// refill masks, barrier counter) | the terminal-observation line mask (lm_words) | k_envq: the
+// refill lanes' plan scratch (gen_off).  Recomputed whenever the image size changes.
+__host__ inline int tail_bytes(const Lds& l) { return kBlock + (l.queue ? 128 : 32) + 4 * l.lm_words; }
+__host__ inline void lds_tail(Lds& l, const DevCfg& c) {
+  // line mask: one bit per 128-byte output line of a whole-workgroup image (<= 64 words), else the
+  // writers test the per-env selection bytes
+  const int64_t total = (int64_t)l.envs * l.seg_bits;
+  const int lines = (int)((127 + total) / 128) + 1;
+  l.lm_words = (!c.need_car && l.sub_envs >= l.envs && lines <= 64 * 32) ? (lines + 31) / 32 : 0;
+  if (const char* e = getenv("PGTG_LINEMASK")) l.lm_words = atoi(e) ? l.lm_words : 0;  // tuning knob
+  l.gen_off = (int)(((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
+                    tail_bytes(l) / 4);
 }
 __host__ inline size_t lds_bytes(const Lds& l) {
   return (size_t)4 * ((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
-         kBlock + (l.queue ? 128 + (size_t)4 * kQueueLanes * l.plan_stride_dw : 32);
+         tail_bytes(l) + (l.queue ? (size_t)4 * kQueueLanes * l.plan_stride_dw : 0);
 }
 
 enum { MODE_STEP = 0, MODE_RESET_SEEDED = 1, MODE_RESET_UNSEEDED = 2, MODE_OBSERVE = 3 };
@@ -1498,13 +1569,12 @@ __device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, con
     const int cnt = min(L.sub_envs, nb - sb);
     if (want && slot >= sb && slot < sb + cnt) {
       ObsInfo oi;
-      build_obs<TR>(c, S, pl, v, st + (slot - sb) * L.seg_words, oi, occ);
+      build_obs<TR>(c, S, pl, v, st, (uint32_t)(slot - sb) * (uint32_t)c.obs_bytes, oi, occ);
       write_small_outputs(c, o, env0 + slot, v, oi, final);
     }
     __syncthreads();
     if (dst)
-      write_obs(dst + (env0 + sb) * (uint64_t)c.obs_bytes, (uint32_t)cnt, (uint32_t)(c.win * c.win),
-                (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel ? sel + sb : nullptr);
+      write_obs(dst + (env0 + sb) * (uint64_t)c.obs_bytes, (uint32_t)cnt, (uint32_t)c.obs_bytes, st, sel ? sel + sb : nullptr);
     __syncthreads();
   }
 }
@@ -1544,6 +1614,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   uint32_t* st = lds + L.envs * (L.plan_stride_dw + L.scratch_dw + L.traf_dw + L.hist_dw);
   uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
   uint64_t* wmask = reinterpret_cast<uint64_t*>(sel + kBlock);     // [4] reset ballot per wave
+  uint32_t* lm = L.lm_words ? reinterpret_cast<uint32_t*>(sel + kBlock + 32) : nullptr;  // terminal lines
   const int xf_off = L.envs * L.plan_stride_dw + ((TR && c.need_car) ? L.envs * L.scratch_dw : 0);
   const int xf_dw = (TR && c.need_car) ? L.traf_dw : L.scratch_dw;
   uint32_t* xf = lds + xf_off + my_slot * xf_dw;  // reset hand-over words
@@ -1574,6 +1645,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
         if (k * 4 + j < L.plan_stride_dw) plan_w[k * 4 + j] = wv[j];
     }
   }
+  for (int k = tid; k < L.lm_words; k += kBlock) lm[k] = 0u;
   __syncthreads();  // sT ready
   if (live && (TR && c.need_car)) {
     // occupancy counters from the current car positions (one coalesced slot row per car index)
@@ -1617,6 +1689,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       if (out.truncated) out.truncated[i] = (v.flags & kFlagTruncated) ? 1 : 0;
       if (out.braking) out.braking[i] = (uint8_t)res.triggered;
       my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
+      if (lm && my_sel && out.final_obs) mark_lines(lm, out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)slot, (uint32_t)c.obs_bytes);
     } else if (mode == MODE_RESET_SEEDED || mode == MODE_RESET_UNSEEDED) {
       const bool do_reset = mask == nullptr || mask[i] != 0;
       if (do_reset && mode == MODE_RESET_SEEDED) v.spawn = 0;
@@ -1651,7 +1724,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (single) {
     if (live && (my_sel != 2)) {
       ObsInfo oi;
-      build_obs<TR>(c, S, pl, v, st + slot * L.seg_words, oi, occ);
+      build_obs<TR>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, occ);
       write_small_outputs(c, out, i, v, oi, my_sel == 1);
     }
     if (L.compact && reset_now) xf[0] = v.spawn;  // after the terminal image read the counters
@@ -1659,8 +1732,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     __syncthreads();
     STAMP(29);
     if (want_final && out.final_obs && !helpers)
-      write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
-                (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel);
+      write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, -1, kBlock, lm);
   } else {
     if (want_final) obs_pass<TR>(c, S, pl, v, out, out.final_obs, env0, nb, my_sel == 1, true, sel, st, L, occ, slot);
     if (L.compact) {
@@ -1673,8 +1745,8 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (!L.compact) n_resets = __syncthreads_count(reset_now);
   if (tid == 0 && n_resets) atomicAdd(&S.counters[1], (unsigned long long)n_resets);
   if (helpers && want_final && out.final_obs && tid >= t_help)
-    write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
-              (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel, tid - t_help, kBlock - t_help);
+    write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, tid - t_help,
+              kBlock - t_help, lm);
   if (L.compact) {
     if (wslot >= 0) {
       uint32_t* xw = lds + xf_off + wslot * xf_dw;
@@ -1750,15 +1822,14 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     if (helpers && !L.compact) __syncthreads();  // the terminal observations are written before slots are rebuilt
     if (reset_now) {
       ObsInfo oi;
-      build_obs<TR>(c, S, pl, v, st + slot * L.seg_words, oi, nullptr);  // cars come from k_traffic
+      build_obs<TR>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);  // cars come from k_traffic
       write_small_outputs(c, out, i, v, oi, false);
     }
     STAMP(30);
     __syncthreads();
     STAMP(31);
     if (out.obs)
-      write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
-                (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, nullptr);
+      write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr);
   } else {
     obs_pass<TR>(c, S, pl, v, out, out.obs, env0, nb, live, false, nullptr, st, L, reset_now ? nullptr : occ,
                  slot);
@@ -1854,6 +1925,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
   uint64_t* fm = reinterpret_cast<uint64_t*>(sel + kBlock);  // [level][env wave]: envs refilled at ring level
   uint32_t* ctr = reinterpret_cast<uint32_t*>(fm + 3 * kQueueDepth);  // sub_barrier counter
+  uint32_t* lm = L.lm_words ? reinterpret_cast<uint32_t*>(sel + kBlock + 128) : nullptr;  // terminal lines
   Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
 
   EnvView v{};
@@ -1881,7 +1953,8 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     }
   }
   if (tid == 0) *ctr = 0u;
-  __syncthreads();  // tables, plans, refill masks, counter
+  for (int k = tid; k < L.lm_words; k += kBlock) lm[k] = 0u;
+  __syncthreads();  // tables, plans, refill masks, counter, line mask
   STAMP(1);
   // refills: the heads of empty rings (level 0, all of them), then levels 1.. in order (the first
   // kQueueLanes this launch; the rest wait for a later launch)
@@ -1940,18 +2013,20 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     if (out.truncated) out.truncated[i] = (v.flags & kFlagTruncated) ? 1 : 0;
     if (out.braking) out.braking[i] = 0;
     my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
+    if (lm && my_sel && out.final_obs) mark_lines(lm, out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)slot, (uint32_t)c.obs_bytes);
     ObsInfo oi;  // the post-step image of every env (terminal for the finished ones)
-    build_obs<false>(c, S, pl, v, st + slot * L.seg_words, oi, nullptr);
+    build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
     write_small_outputs(c, out, i, v, oi, my_sel == 1);
   }
   if (env_wave) sel[slot] = my_sel;
   const uint64_t rm = __ballot(my_sel == 1);
   if (env_wave && lane == 0 && rm) atomicAdd(&S.counters[1], (unsigned long long)__popcll(rm));
   STAMP(2);
+  STAMP(28);
   sub_barrier(ctr, (uint32_t)np);
+  STAMP(29);
   if (out.final_obs)
-    write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
-              (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, sel, rank, nthr);
+    write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, rank, nthr, lm);
   STAMP(3);
   sub_barrier(ctr, 2u * np);  // terminal images written before they are rebuilt
   if (any_empty) __syncthreads();  // the head refills
@@ -2017,15 +2092,14 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   STAMP(5);
   if (reset_now) {
     ObsInfo oi;
-    build_obs<false>(c, S, pl, v, st + slot * L.seg_words, oi, nullptr);
+    build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
     write_small_outputs(c, out, i, v, oi, false);
   }
   STAMP(30);
   sub_barrier(ctr, 3u * np);
   STAMP(31);
   if (out.obs)
-    write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)(c.win * c.win),
-              (uint32_t)c.mask_words, (uint32_t)c.n_channels, st, nullptr, rank, nthr);
+    write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr, rank, nthr);
   if (tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
   STAMP(6);
 }
@@ -2658,7 +2732,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
       auto shrink = [&](Lds l) {
         while (l.sub_envs > 8 && lds_bytes(l) + sizeof(Tables) > 80 * 1024) {
           l.sub_envs /= 2;
-          l.stream_words = l.sub_envs * l.seg_words + 2;
+          l.stream_words = img_words(l.sub_envs, l.seg_bits);
         }
         return l;
       };
@@ -2675,14 +2749,14 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
       auto fit = [&](const Lds& l) { return (int)((160 * 1024) / (lds_bytes(l) + sizeof(Tables))); };
       while (fit(h->L) < want && h->L.sub_envs > 64) {
         h->L.sub_envs /= 2;
-        h->L.stream_words = h->L.sub_envs * h->L.seg_words + 2;
+        h->L.stream_words = img_words(h->L.sub_envs, h->L.seg_bits);
       }
     }
     if (const char* e = getenv("PGTG_OBS_SUB")) {  // tuning knob: observation sub-batch size
       int sub = atoi(e);
       if (sub >= 1 && sub < h->L.sub_envs) {
         h->L.sub_envs = sub;
-        h->L.stream_words = sub * h->L.seg_words + 2;
+        h->L.stream_words = img_words(sub, h->L.seg_bits);
       }
     }
     if (c.need_car) {
@@ -2704,9 +2778,11 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
   }
   // map queue (k_envq): recheck after the adjustments above, place the helper scratch, allocate
   h->L.queue = h->L.queue && h->L.sub_envs >= h->L.envs && h->L.envs <= kBlock - 64;
-  h->L.gen_off = (int)(((size_t)h->L.envs * (h->L.plan_stride_dw + h->L.scratch_dw + h->L.traf_dw + h->L.hist_dw) +
-                        h->L.stream_words) + (kBlock + 128) / 4);
-  if (h->L.queue && lds_bytes(h->L) + sizeof(Tables) > 40 * 1024) h->L.queue = 0;  // keep 4 workgroups per CU
+  lds_tail(h->L, c);
+  if (h->L.queue && lds_bytes(h->L) + sizeof(Tables) > 40 * 1024) {  // keep 4 workgroups per CU
+    h->L.queue = 0;
+    lds_tail(h->L, c);
+  }
   if (h->L.queue) {
     if ((rc = dalloc(h, &h->S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw)) || (rc = dalloc(h, &h->S.qstate, n))) {
       g_create_err = h->err;

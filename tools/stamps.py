@@ -27,6 +27,7 @@ SUB = {"cars": (16, 17), "braking": (17, 18), "reset.seed": (8, 9), "reset.gener
        "obs.rebuild": (5, 30), "obs.barrier": (30, 31), "obs.write": (31, 6)}
 CASES = {"cfg2": (4096, dict(random_map_width=3, random_map_height=3)),
          "cfg5": (131072, dict(random_map_width=5, random_map_height=5)),
+         "cfg4": (262144, dict(random_map_width=3, random_map_height=3)),
          "cfg3": (65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5))}
 for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
     N, kw = CASES[name]
@@ -57,6 +58,8 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
     d = np.diff(st[:, :7], axis=1)
     print(f"{name}: {N} envs, {E} envs/workgroup, LDS {lds} B; cycles per active wave (last launch)", flush=True)
     print("  phases:", {n: int(x) for n, x in zip(PHASES, d.mean(0))}, "total", int((st[:, 6] - st[:, 0]).mean()))
+    print("  phase p90/max:", {n: (int(np.percentile(d[:, k], 90)), int(d[:, k].max())) for k, n in enumerate(PHASES)},
+          "total max", int((st[:, 6] - st[:, 0]).max()))
     lo, hi = st[:, 0], st[:, 6]
     out = {}
     for n, (a, b) in SUB.items():
