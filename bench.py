@@ -175,7 +175,7 @@ def main():
             "episodes": total_eps,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": load_traffic(args.workload, alg),
-                         "kernel": "pgtg::k_env (step + auto-reset)", "avg_kernel_us": avg_kernel_s * 1e6,
+                         "kernel": env.step_kernel() + " (step + in-kernel auto-reset)", "avg_kernel_us": avg_kernel_s * 1e6,
                          "alg_bytes_per_launch": alg, "resets_per_launch": resets_per_launch,
                          "envs_per_workgroup": env.launch_info()[0], "lds_bytes": env.launch_info()[1],
                          "workgroups_per_cu": env.occupancy()},

@@ -195,6 +195,8 @@ uint64_t pgtg_num_envs(const pgtg_handle* h);
 int pgtg_launch_info(const pgtg_handle* h, int32_t* envs_per_block, int32_t* lds_bytes);
 /* Resident workgroups per CU of the step kernel this handle launches (HIP occupancy query). */
 int pgtg_occupancy(const pgtg_handle* h, int32_t* step_blocks_per_cu);
+/* Name of the kernel(s) one pgtg_step launches for this handle (measurement labels). */
+const char* pgtg_step_kernel(const pgtg_handle* h);
 const char* pgtg_last_error(const pgtg_handle* h);
 /* Per-launch device timing of the step kernels with HIP events on the handle's stream.  every > 0:
  * every every-th pgtg_step brackets its kernels with an event pair (1: all; 0: off);

@@ -30,7 +30,7 @@ EXPORTED = [
     "pgtg_create", "pgtg_destroy", "pgtg_set_stream", "pgtg_set_outputs", "pgtg_reset",
     "pgtg_reset_unseeded", "pgtg_step", "pgtg_random_actions", "pgtg_get_env_state", "pgtg_get_cars",
     "pgtg_get_map_plan", "pgtg_get_squares", "pgtg_set_rules", "pgtg_set_agent", "pgtg_add_car", "pgtg_observe", "pgtg_get_counters",
-    "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_launch_info", "pgtg_occupancy", "pgtg_last_error", "pgtg_enable_timing",
+    "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_launch_info", "pgtg_occupancy", "pgtg_step_kernel", "pgtg_last_error", "pgtg_enable_timing",
     "pgtg_timing_read",
 ]
 
@@ -123,6 +123,7 @@ def lib():
         "pgtg_num_envs": ([vp], u64),
         "pgtg_launch_info": ([vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
         "pgtg_occupancy": ([vp, C.POINTER(i32)], C.c_int),
+        "pgtg_step_kernel": ([vp], C.c_char_p),
         "pgtg_last_error": ([vp], C.c_char_p),
         "pgtg_timing_read": ([vp, C.POINTER(C.c_double), C.POINTER(u64), i32], C.c_int),
         "pgtg_enable_timing": ([vp, i32], C.c_int),

@@ -39,7 +39,72 @@ namespace hs {
 #undef PGTG_TBL_QUAL
 }  // namespace hs
 
-__shared__ Tables sT;  // per-workgroup LDS copy of the lane-indexed tables
+__shared__ __attribute__((aligned(16))) Tables sT;  // per-workgroup LDS copy of the lane-indexed tables
+
+// Copy the first `bytes` of the tables into sT: all of a thread's 16-byte loads are issued before
+// the first LDS store (one memory latency instead of one per word).
+__device__ __forceinline__ void stage_tables(const Tables* __restrict__ gtab, int bytes) {
+#ifdef PGTG_OLD_STAGE  // A/B build only
+  for (int k = threadIdx.x; k < bytes / 4; k += kBlock)
+    reinterpret_cast<uint32_t*>(&sT)[k] = reinterpret_cast<const uint32_t*>(gtab)[k];
+  return;
+#endif
+  const int n4 = bytes >> 4, tid = (int)threadIdx.x;
+  const uint4* src = reinterpret_cast<const uint4*>(gtab);
+  uint4* dst = reinterpret_cast<uint4*>(&sT);
+  uint4 r[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+    if (tid + j * kBlock < n4) r[j] = src[tid + j * kBlock];
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+    if (tid + j * kBlock < n4) dst[tid + j * kBlock] = r[j];
+  for (int k = tid + 4 * kBlock; k < n4; k += kBlock) dst[k] = src[k];
+  for (int k = n4 * 4 + tid; k < bytes / 4; k += kBlock)
+    reinterpret_cast<uint32_t*>(&sT)[k] = reinterpret_cast<const uint32_t*>(gtab)[k];
+}
+
+// Workgroup barrier for LDS data only: unlike __syncthreads() it does not wait for the waves'
+// outstanding global stores (outputs, state) to complete.
+__device__ __forceinline__ void lds_barrier() {
+#ifdef PGTG_FULL_FENCE  // A/B build only
+  __syncthreads();
+#else
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#endif
+}
+
+// One env's tile plan (plan_stride u16 words in HBM, a multiple of 8, <= 64) into its LDS row of
+// pdw words, all loads first.
+__device__ __forceinline__ void stage_plan(const uint16_t* __restrict__ plan, int plan_stride, uint32_t* dst, int pdw) {
+  const uint4* src = reinterpret_cast<const uint4*>(plan);
+  const int nq = plan_stride / 8;
+#ifdef PGTG_OLD_STAGE  // A/B build only
+  for (int k = 0; k < nq; k++) {
+    const uint4 w4 = src[k];
+    const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (k * 4 + j < pdw) dst[k * 4 + j] = wv[j];
+  }
+  return;
+#endif
+  uint4 q[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    if (k < nq) q[k] = src[k];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (k < nq) {
+      const uint32_t wv[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (k * 4 + j < pdw) dst[k * 4 + j] = wv[j];
+    }
+  }
+}
 
 // Diagnostic build only (-DPGTG_STAMPS): per-wave phase timestamps (s_memtime) into a debug buffer
 // that nothing else reads.  The product build compiles these to nothing.
@@ -1572,10 +1637,10 @@ __device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, con
       build_obs<TR>(c, S, pl, v, st, (uint32_t)(slot - sb) * (uint32_t)c.obs_bytes, oi, occ);
       write_small_outputs(c, o, env0 + slot, v, oi, final);
     }
-    __syncthreads();
+    lds_barrier();
     if (dst)
       write_obs(dst + (env0 + sb) * (uint64_t)c.obs_bytes, (uint32_t)cnt, (uint32_t)c.obs_bytes, st, sel ? sel + sb : nullptr);
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -1592,12 +1657,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   // the traffic-reset list of the next launch starts empty (its previous consumer has finished)
   if ((TR && c.need_car) && mode != MODE_OBSERVE && blockIdx.x == 0 && tid == 0) S.tr_count[tr_slot ^ 1u] = 0u;
   // stage the lane-indexed tables (kLanes only when a pass needs it)
-  {
-    const int words = (int)((c.generic_channels || (TR && c.need_car) ? sizeof(Tables) : offsetof(Tables, lanes)) / 4);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
-    uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
-    for (int k = tid; k < words; k += blockDim.x) dstt[k] = src[k];
-  }
+  stage_tables(gtab, (int)(c.generic_channels || (TR && c.need_car) ? sizeof(Tables) : offsetof(Tables, lanes)));
   const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
   const int nb = (int)min((uint64_t)L.envs, S.n - env0);
   // env slots: E/4 per wave when a workgroup holds fewer than 256 envs, so that all four SIMDs
@@ -1636,17 +1696,10 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       ts.next_id = tr4.y;
       ts.bank = tr4.z;
     }
-    const uint4* src = reinterpret_cast<const uint4*>(S.plan + i * (uint64_t)c.plan_stride);
-    for (int k = 0; k < c.plan_stride / 8; k++) {
-      uint4 w4 = src[k];
-      uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (k * 4 + j < L.plan_stride_dw) plan_w[k * 4 + j] = wv[j];
-    }
+    stage_plan(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, L.plan_stride_dw);
   }
   for (int k = tid; k < L.lm_words; k += kBlock) lm[k] = 0u;
-  __syncthreads();  // sT ready
+  lds_barrier();  // sT ready
   if (live && (TR && c.need_car)) {
     // occupancy counters from the current car positions (one coalesced slot row per car index)
     for (int w = 0; w < c.nt * 4; w++) traf_w[w] = 0u;  // 16 B of 4-bit counters per tile
@@ -1704,7 +1757,14 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     const uint64_t m = __ballot(reset_now);
     if ((tid & 63) == 0) wmask[tid >> 6] = m;
   }
-  const int n_final = __syncthreads_count(my_sel == 1);
+  int n_final = 0;
+  if (L.compact) {  // step launches: every reset is a finished episode (my_sel == 1)
+    lds_barrier();
+    if (mode == MODE_STEP)
+      for (int w = 0; w < kBlock / 64; w++) n_final += __popcll(wmask[w]);
+  } else {
+    n_final = __syncthreads_count(my_sel == 1);
+  }
   const bool want_final = mode == MODE_STEP && n_final && (out.final_obs || out.final_position || out.final_velocity);
   int n_resets = 0, wslot = -1;
   if (L.compact) {
@@ -1729,7 +1789,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     }
     if (L.compact && reset_now) xf[0] = v.spawn;  // after the terminal image read the counters
     STAMP(28);
-    __syncthreads();
+    lds_barrier();
     STAMP(29);
     if (want_final && out.final_obs && !helpers)
       write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, -1, kBlock, lm);
@@ -1737,7 +1797,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     if (want_final) obs_pass<TR>(c, S, pl, v, out, out.final_obs, env0, nb, my_sel == 1, true, sel, st, L, occ, slot);
     if (L.compact) {
       if (reset_now) xf[0] = v.spawn;
-      __syncthreads();
+      lds_barrier();
     }
   }
   STAMP(3);
@@ -1767,7 +1827,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       xw[1] = vv.sg;
       xw[2] = vv.path_len | (uint32_t)(-e2) << 16;
     }
-    __syncthreads();  // hand-over words ready (and the terminal observations written)
+    lds_barrier();  // hand-over words ready (and the terminal observations read from the image)
     if (reset_now) {  // env_reset's state on the env's own lane
       const uint32_t x0 = xf[0], x2 = xf[2];
       v.px = (int)(int16_t)(x0 & 0xffffu);
@@ -1819,14 +1879,14 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   }
   STAMP(5);
   if (single) {
-    if (helpers && !L.compact) __syncthreads();  // the terminal observations are written before slots are rebuilt
+    if (helpers && !L.compact) lds_barrier();  // the terminal observations are written before slots are rebuilt
     if (reset_now) {
       ObsInfo oi;
       build_obs<TR>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);  // cars come from k_traffic
       write_small_outputs(c, out, i, v, oi, false);
     }
     STAMP(30);
-    __syncthreads();
+    lds_barrier();
     STAMP(31);
     if (out.obs)
       write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr);
@@ -1885,11 +1945,21 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
 // Barrier among the waves of a workgroup that take part (lane 0 of each arrives at an LDS counter
 // that only grows; `target` = uses so far x participating waves), for phases that must not wait
 // for a wave busy elsewhere.
+// LDS-only fences: the waves exchange LDS data only, so their global stores stay in flight across
+// the barrier (a plain workgroup fence waits for every outstanding global access first).
 __device__ __forceinline__ void sub_barrier(uint32_t* ctr, uint32_t target) {
+#ifdef PGTG_FULL_FENCE  // A/B build only
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#else
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+#endif
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+#ifdef PGTG_FULL_FENCE
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#endif
 }
 
 // Step launch with the map queue (no traffic; workgroups of <= 192 envs).  Wave `env_waves` (the
@@ -1905,12 +1975,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   const DevCfg& c = *cfg;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   STAMP(0);
-  {
-    const int words = (int)((c.generic_channels ? sizeof(Tables) : offsetof(Tables, lanes)) / 4);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
-    uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
-    for (int k = tid; k < words; k += blockDim.x) dstt[k] = src[k];
-  }
+  stage_tables(gtab, (int)(c.generic_channels ? sizeof(Tables) : offsetof(Tables, lanes)));
   const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
   const int nb = (int)min((uint64_t)L.envs, S.n - env0);
   const int env_waves = (L.envs + 63) / 64, gen_wave = env_waves;
@@ -1933,14 +1998,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   if (live) {
     v = rec_load(S.rec, i);
     qs = S.qstate[i];
-    const uint4* src = reinterpret_cast<const uint4*>(S.plan + i * (uint64_t)c.plan_stride);
-    for (int k = 0; k < c.plan_stride / 8; k++) {
-      uint4 w4 = src[k];
-      uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (k * 4 + j < pdw) plan_w[k * 4 + j] = wv[j];
-    }
+    stage_plan(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, pdw);
     xf[slot * L.scratch_dw] = v.spawn;
     xf[slot * L.scratch_dw + 1] = qs;
   }
@@ -1954,7 +2012,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   }
   if (tid == 0) *ctr = 0u;
   for (int k = tid; k < L.lm_words; k += kBlock) lm[k] = 0u;
-  __syncthreads();  // tables, plans, refill masks, counter, line mask
+  lds_barrier();  // tables, plans, refill masks, counter, line mask
   STAMP(1);
   // refills: the heads of empty rings (level 0, all of them), then levels 1.. in order (the first
   // kQueueLanes this launch; the rest wait for a later launch)
@@ -2158,26 +2216,14 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
   const int tid0 = threadIdx.x;
   const bool has_slot = (tid0 & 63) < per_wave;
   const int tid = has_slot ? (tid0 >> 6) * per_wave + (tid0 & 63) : 0;
-  {
-    const int words = (int)(sizeof(Tables) / 4);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
-    uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
-    for (int k = tid0; k < words; k += blockDim.x) dstt[k] = src[k];
-  }
+  stage_tables(gtab, (int)sizeof(Tables));
   __syncthreads();
   const uint32_t j = j0 + tid;
   if (!has_slot || j >= n) return;
   const uint64_t i = S.tr_list[j];
   uint32_t* plan_w = lds + tid * plan_dw;
   uint8_t* rs = reinterpret_cast<uint8_t*>(lds + lanes * plan_dw + tid * rs_dw);
-  const uint4* src = reinterpret_cast<const uint4*>(S.plan + i * (uint64_t)c.plan_stride);
-  for (int k = 0; k < c.plan_stride / 8; k++) {
-    uint4 w4 = src[k];
-    uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-      if (k * 4 + q < plan_dw) plan_w[k * 4 + q] = wv[q];
-  }
+  stage_plan(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, plan_dw);
   Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
   const EnvView v = rec_load(S.rec, i);
   const int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
@@ -3140,6 +3186,13 @@ int pgtg_read_stamps(uint64_t* out, uint64_t n) {
 
 int pgtg_window(const pgtg_handle* h) { return h ? h->hcfg.win : 0; }
 uint64_t pgtg_num_envs(const pgtg_handle* h) { return h ? h->n : 0; }
+const char* pgtg_step_kernel(const pgtg_handle* h) {
+  if (!h) return "";
+  if (h->hcfg.need_car) return "pgtg::k_env<true> + pgtg::k_traffic";
+  if (h->hcfg.n_rules > 0) return "pgtg::k_env<true>";
+  return h->L.queue ? "pgtg::k_envq" : "pgtg::k_env<false>";
+}
+
 int pgtg_occupancy(const pgtg_handle* h, int32_t* step_blocks_per_cu) {
   if (!h) return PGTG_E_INVALID;
   int nb = 0;

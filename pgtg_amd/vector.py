@@ -285,6 +285,10 @@ class PGTGVecEnv:
         _check(self._lib.pgtg_occupancy(self._h, C.byref(n)), self._h)
         return n.value
 
+    def step_kernel(self) -> str:
+        """Name of the kernel(s) a step launches (measurement labels)."""
+        return self._lib.pgtg_step_kernel(self._h).decode()
+
     def counters(self) -> tuple[int, int]:
         a, b = C.c_uint64(), C.c_uint64()
         _check(self._lib.pgtg_get_counters(self._h, C.byref(a), C.byref(b)), self._h)
