@@ -2023,6 +2023,11 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     for (int w = 0; w < env_waves; w++) F[l] += __popcll(fm[l * 3 + w]);
   }
   const bool any_empty = F[0] != 0;
+#ifdef PGTG_STAMPS
+  if ((threadIdx.x & 63) == 0)  // diagnostic: empty rings and level-1/2 refills wanted in this workgroup
+    g_stamps[((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 32 + 12) & ((1 << 21) - 1)] =
+        (unsigned long long)F[0] | (unsigned long long)F[1] << 16 | (unsigned long long)F[2] << 32;
+#endif
 
   if (wave == gen_wave) {
     uint16_t* gplan = reinterpret_cast<uint16_t*>(lds + L.gen_off + lane * pdw);
@@ -2049,6 +2054,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
         l++;
       }
       if (l < kQueueDepth) refill(k, l);
+      if (L.diag == 8 && l < kQueueDepth) refill(k, l);  // diagnostic: the same (deterministic) refill twice
     }
     STAMP(7);
     return;
@@ -2074,6 +2080,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     if (lm && my_sel && out.final_obs) mark_lines(lm, out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)slot, (uint32_t)c.obs_bytes);
     ObsInfo oi;  // the post-step image of every env (terminal for the finished ones)
     build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
+    if (L.diag == 9) build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);  // diagnostic
     write_small_outputs(c, out, i, v, oi, my_sel == 1);
   }
   if (env_wave) sel[slot] = my_sel;
