@@ -54,8 +54,7 @@ __device__ __forceinline__ void stage_tables(const Tables* __restrict__ gtab, in
   uint4* dst = reinterpret_cast<uint4*>(&sT);
   uint4 r[4];
 #pragma unroll
-  for (int j = 0; j < 4; j++)
-    if (tid + j * kBlock < n4) r[j] = src[tid + j * kBlock];
+  for (int j = 0; j < 4; j++) r[j] = src[tid + j * kBlock < n4 ? tid + j * kBlock : 0];  // unconditional: registers, not scratch
 #pragma unroll
   for (int j = 0; j < 4; j++)
     if (tid + j * kBlock < n4) dst[tid + j * kBlock] = r[j];
@@ -93,8 +92,7 @@ __device__ __forceinline__ void stage_plan(const uint16_t* __restrict__ plan, in
 #endif
   uint4 q[8];
 #pragma unroll
-  for (int k = 0; k < 8; k++)
-    if (k < nq) q[k] = src[k];
+  for (int k = 0; k < 8; k++) q[k] = src[k < nq ? k : 0];  // unconditional: registers, not scratch
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     if (k < nq) {
@@ -2819,6 +2817,10 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
       h->kt_lanes = 64;
       while (h->kt_lanes > 4 && (size_t)4 * h->kt_lanes * (h->kt_plan_dw + h->kt_rs_dw) + sizeof(Tables) > 150 * 1024)
         h->kt_lanes /= 2;
+      if (const char* e = getenv("PGTG_KT_LANES")) {  // tuning knob: envs per k_traffic workgroup
+        const int want = atoi(e);
+        if (want >= 4 && want <= h->kt_lanes && (want & (want - 1)) == 0) h->kt_lanes = want;
+      }
       h->kt_lds = (size_t)4 * h->kt_lanes * (h->kt_plan_dw + h->kt_rs_dw);
       if (h->kt_lds + sizeof(Tables) > 160 * 1024) {
         g_create_err = "LDS budget exceeded (traffic reset scratch)";
