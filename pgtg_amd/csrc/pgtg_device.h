@@ -78,6 +78,7 @@ struct DevCfg {
   int32_t rs_bytes;        // k_traffic per-lane reset scratch: Floyd output [0, 2*cap), seen set, column prefix
   int32_t rs_seen_off;
   int32_t rs_pre_off;
+  int32_t rs_cm_off;        // per-column masks of spawnable rows (u32 pairs; maps of <= 7 tile rows, else 0)
   int32_t traffic_ch;      // index of the traffic channel in the observation, -1 if absent
   int32_t obs_fast;        // observation window == the agent's tile (k_traffic patches its traffic bits)
   int32_t manual_cars;     // cars may be added through pgtg_add_car

@@ -649,24 +649,60 @@ __device__ __forceinline__ uint32_t spawner_colmask(const DevCfg& c, uint32_t ex
   return m;
 }
 
+// Lanes of one wave exchanging LDS data: the wave's LDS accesses complete in program order, so a
+// compiler fence at wavefront scope is all the ordering they need.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
 // Initial traffic of a fresh episode (EpisodeMap scans pgtg/map.py:31-42 and
 // _create_initial_traffic pgtg/environment.py:830-879), run by k_traffic for the envs k_env reset.
-// `rs` is the lane's LDS reset scratch: Floyd's output [0, 2*cap), its seen set and the per-column
-// prefix of spawnable squares.  CR collects the new cars on the agent's tile `at` (observation).
+// `g` (1..4) adjacent lanes of a wave share one env (`sub` 0..g-1): lane 0 runs the serial parts
+// (Floyd's choice, the shuffle, the per-car draws in id order); the sweep and the square lookup of
+// every chosen index, which have no RNG and no order, are split over the group.  `rs` is the env's LDS reset scratch:
+// Floyd's output [0, 2*cap) (then the chosen square codes), its seen set and the per-column prefix
+// of spawnable squares.  CR collects the new cars on the agent's tile `at` (observation); lane 0's
+// return value, state and CR are the result.
 __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S, uint64_t i, const Plan& pl,
-                                             Pcg& cr, uint8_t* rs, TrafState& ts, int at, uint32_t* CR) {
+                                             Pcg& cr, uint8_t* rs, TrafState& ts, int at, uint32_t* CR, int sub,
+                                             int g) {
   const uint64_t N = S.n;
   STAMP(19);
-  // one x-major sweep: car spawners -> HBM list, spawnable squares (any car lane) -> per-column
-  // prefix counts
+  // x-major sweep, the group's lanes on g column ranges: count, exchange the counts, then car
+  // spawners -> HBM list and spawnable squares (any car lane) -> per-column prefix counts
   uint16_t* colpre = reinterpret_cast<uint16_t*>(rs + c.rs_pre_off);
-  int nsp = 0, np = 0;
-  for (int x = 0; x < c.W; x++) {
+  const int xa = c.W * sub / g, xb = c.W * (sub + 1) / g;
+  int cnp = 0, cnsp = 0;
+  for (int x = xa; x < xb; x++) {
     const int tx = x / kTile, lx = x - tx * kTile;
-    colpre[x] = (uint16_t)np;
     for (int ty = 0; ty < c.th; ty++) {
       const uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
-      np += __popc(sT.lanecol[ex][lx]);  // row 0 (no exits) is empty
+      cnp += __popc(sT.lanecol[ex][lx]);  // row 0 (no exits) is empty
+      cnsp += __popc(spawner_colmask(c, ex, tx, ty, lx));
+    }
+  }
+  const int q0 = (int)(threadIdx.x & 63u) - sub;
+  int np = 0, nsp = 0, tot_np = 0, tot_nsp = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int a = __shfl(cnp, q0 + (j < g ? j : 0)), b = __shfl(cnsp, q0 + (j < g ? j : 0));
+    np += j < sub ? a : 0;
+    nsp += j < sub ? b : 0;
+    tot_np += j < g ? a : 0;
+    tot_nsp += j < g ? b : 0;
+  }
+  uint32_t* colm = c.rs_cm_off ? reinterpret_cast<uint32_t*>(rs + c.rs_cm_off) : nullptr;
+  for (int x = xa; x < xb; x++) {
+    const int tx = x / kTile, lx = x - tx * kTile;
+    colpre[x] = (uint16_t)np;
+    uint64_t cm = 0;
+    for (int ty = 0; ty < c.th; ty++) {
+      const uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
+      const uint32_t lc = sT.lanecol[ex][lx];
+      np += __popc(lc);
+      cm |= (uint64_t)lc << (9 * (ty & 7));
       uint32_t m = spawner_colmask(c, ex, tx, ty, lx);
       while (m) {
         int ly = __ffs((int)m) - 1;
@@ -675,8 +711,15 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
         nsp++;
       }
     }
+    if (colm) {
+      colm[2 * x] = (uint32_t)cm;
+      colm[2 * x + 1] = (uint32_t)(cm >> 32);
+    }
   }
-  colpre[c.W] = (uint16_t)np;
+  np = tot_np;
+  nsp = tot_nsp;
+  if (sub == g - 1) colpre[c.W] = (uint16_t)np;
+  wave_lds_sync();
   const int ncars = (int)((double)np * c.density);  // int(len(positions) * traffic_density)
   int k = 0;
   CarStore cs{S.car_w0, S.car_w1, S.car_id, N, i};
@@ -684,26 +727,30 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
     k = min(ncars, np);
     if (k > c.car_cap) return PGTG_E_UNSUPPORTED;
     uint16_t* out = reinterpret_cast<uint16_t*>(rs);
-    uint32_t* seen = reinterpret_cast<uint32_t*>(rs + c.rs_seen_off);
-    for (int w = 0; w < (np + 31) / 32; w++) seen[w] = 0u;
-    STAMP(20);
-    // Generator.choice(np, k, replace=False): Floyd's algorithm, then _shuffle_int
-    for (int j = np - k; j < np; j++) {
-      int val = (int)pcg_int(cr, (uint32_t)(j + 1));
-      if ((seen[val >> 5] >> (val & 31)) & 1u) val = j;
-      seen[val >> 5] |= 1u << (val & 31);
-      out[j - (np - k)] = (uint16_t)val;
+    if (sub == 0) {
+      uint32_t* seen = reinterpret_cast<uint32_t*>(rs + c.rs_seen_off);
+      for (int w = 0; w < (np + 31) / 32; w++) seen[w] = 0u;
+      STAMP(20);
+      // Generator.choice(np, k, replace=False): Floyd's algorithm, then _shuffle_int
+      for (int j = np - k; j < np; j++) {
+        int val = (int)pcg_int(cr, (uint32_t)(j + 1));
+        if ((seen[val >> 5] >> (val & 31)) & 1u) val = j;
+        seen[val >> 5] |= 1u << (val & 31);
+        out[j - (np - k)] = (uint16_t)val;
+      }
+      STAMP(21);
+      for (int m = k - 1; m >= 1; m--) {
+        int jj = (int)pcg_int(cr, (uint32_t)(m + 1));
+        const uint16_t t = out[m], u = out[jj];
+        out[m] = u;
+        out[jj] = t;
+      }
     }
-    STAMP(21);
-    for (int m = k - 1; m >= 1; m--) {
-      int jj = (int)pcg_int(cr, (uint32_t)(m + 1));
-      const uint16_t t = out[m], u = out[jj];
-      out[m] = u;
-      out[jj] = t;
-    }
+    wave_lds_sync();
     STAMP(22);
     const int tw = c.tw, th = c.th;
-    for (int m = 0; m < k; m++) {
+    // the group looks up the squares: chosen index -> square code x | y << 8 in place
+    for (int m = sub; m < k; m += g) {
       const int idx = out[m];
       // column: the tile column from the prefixes at tile-column starts, then the column inside it
       int tx = 0;
@@ -713,22 +760,56 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
 #pragma unroll
       for (int j = 1; j < kTile; j++) lx += cp[j] <= idx ? 1 : 0;
       // row: the tile of the column holding the rr-th spawnable square (no early exit)
-      int rr = idx - cp[lx], ty_f = 0, rr_f = 0;
-      uint32_t ex_f = 0, msk_f = 0;
-      for (int ty = 0; ty < th; ty++) {
-        const uint32_t ex = plan_exits(pl[ty * tw + tx]);
-        const uint32_t msk = sT.lanecol[ex][lx];
-        const int cnt = __popc(msk);
-        if (rr >= 0 && rr < cnt) {
-          ty_f = ty;
-          ex_f = ex;
-          msk_f = msk;
-          rr_f = rr;
+      int rr = idx - cp[lx];
+      const int x = tx * kTile + lx;
+      int y;
+      if (colm) {  // the rr-th set bit of the column mask
+        uint32_t w = colm[2 * x];
+        const uint32_t hi = colm[2 * x + 1];
+        int base = 0;
+        const int c32 = __popc(w);
+        if (rr >= c32) {
+          rr -= c32;
+          w = hi;
+          base = 32;
         }
-        rr -= cnt;
+#pragma unroll
+        for (int sh = 16; sh >= 1; sh >>= 1) {
+          const int cs = __popc(w & ((1u << sh) - 1u));
+          if (rr >= cs) {
+            rr -= cs;
+            w >>= sh;
+            base += sh;
+          }
+        }
+        y = base;
+      } else {  // row: the tile of the column holding the rr-th spawnable square (no early exit)
+        int ty_f = 0, rr_f = 0;
+        uint32_t msk_f = 0;
+        for (int ty = 0; ty < th; ty++) {
+          const uint32_t msk = sT.lanecol[plan_exits(pl[ty * tw + tx])][lx];
+          const int cnt = __popc(msk);
+          if (rr >= 0 && rr < cnt) {
+            ty_f = ty;
+            msk_f = msk;
+            rr_f = rr;
+          }
+          rr -= cnt;
+        }
+        y = ty_f * kTile + kth_bit(msk_f, rr_f);
       }
-      const int ly = kth_bit(msk_f, rr_f);
-      const int x = tx * kTile + lx, y = ty_f * kTile + ly, sq = lx * 9 + ly;
+      out[m] = (uint16_t)(x | y << 8);
+    }
+    wave_lds_sync();
+    STAMP(26);  // (slot shared with k_env's removal-loop record: k_traffic runs later)
+    if (sub != 0) return 0;
+    // the cars in id order: profile and route draws
+    for (int m = 0; m < k; m++) {
+      const uint32_t code = out[m];
+      const int x = (int)(code & 255u), y = (int)(code >> 8);
+      const int tx = (int)((uint32_t)x / (uint32_t)kTile), ty_f = (int)((uint32_t)y / (uint32_t)kTile);
+      const int lx = x - tx * kTile, ly = y - ty_f * kTile, sq = lx * 9 + ly;
+      const uint32_t ex_f = plan_exits(pl[ty_f * tw + tx]);
       if (ty_f * tw + tx == at) CR[sq >> 5] |= 1u << (sq & 31);
       const uint32_t rl = sT.lanes[ex_f][sq] & 0x0fffffffu;
       const uint32_t nr = __popc(rl);
@@ -2206,52 +2287,64 @@ __global__ void __launch_bounds__(kBlock) k_gen_bench(const DevCfg* __restrict__
 }
 #endif
 
-// Initial traffic of the envs k_env reset in this launch (its work list), one lane per env with
-// the reset scratch in LDS; the observation k_env wrote for them gets the new cars' squares.
-// `lanes` envs per 256-lane workgroup, lanes/4 per wave (all four SIMDs, narrower divergence).
+// Initial traffic of the envs k_env reset in this launch (its work list) with the reset scratch in
+// LDS; the observation k_env wrote for them gets the new cars' squares.  One workgroup per CU, and
+// the list is spread evenly over all of their waves: a wave's time is its envs' serial chain whatever
+// the number of active lanes, so the envs per wave are levelled first (`e`, at most `cap_w` in LDS
+// at once, in rounds beyond that), then the wave's 64 lanes are shared out: 4 per env up to 16
+// envs, 3 up to 21, 2 up to 32 (traffic_reset splits the sweep and the square lookup over them).
 __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
                                                     DevState S, PgtgOutputs out, uint32_t tr_slot, int plan_dw,
-                                                    int rs_dw, int lanes) {
+                                                    int rs_dw, int cap_w) {
   extern __shared__ uint32_t lds[];
   const DevCfg& c = *cfg;
   const uint32_t n = S.tr_count[tr_slot];
-  const uint32_t j0 = blockIdx.x * (uint32_t)lanes;
-  if (j0 >= n) return;  // whole workgroup idle
-  const int per_wave = lanes / 4;
-  const int tid0 = threadIdx.x;
-  const bool has_slot = (tid0 & 63) < per_wave;
-  const int tid = has_slot ? (tid0 >> 6) * per_wave + (tid0 & 63) : 0;
+  const uint32_t W = gridDim.x * (kBlock / 64);  // waves of the grid
+  const uint32_t rounds = (n + W * (uint32_t)cap_w - 1) / (W * (uint32_t)cap_w);
+  if (rounds == 0) return;
+  const uint32_t e = (n + W * rounds - 1) / (W * rounds);  // envs per wave and round, <= cap_w
+  if ((uint64_t)blockIdx.x * (kBlock / 64) * e >= n) return;  // whole workgroup idle
+  const int g = e <= 16 ? 4 : (e <= 21 ? 3 : (e <= 32 ? 2 : 1));
+  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
+  const int slot = lane / g, sub = lane - slot * g;
   stage_tables(gtab, (int)sizeof(Tables));
   __syncthreads();
-  const uint32_t j = j0 + tid;
-  if (!has_slot || j >= n) return;
-  const uint64_t i = S.tr_list[j];
-  uint32_t* plan_w = lds + tid * plan_dw;
-  uint8_t* rs = reinterpret_cast<uint8_t*>(lds + lanes * plan_dw + tid * rs_dw);
-  stage_plan(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, plan_dw);
-  Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
-  const EnvView v = rec_load(S.rec, i);
-  const int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
-  const int at = (piy / kTile) * c.tw + pix / kTile;
-  Pcg cr = stream_load(S.car, i);
-  TrafState ts{0, 0, 0, 0};
-  uint32_t CR[3] = {0u, 0u, 0u};
-  const int e = traffic_reset(c, S, i, pl, cr, rs, ts, at, CR);
-  stream_store_state(S.car, i, cr);
-  S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.bank, 0u);
-  if (e) S.err[i] = (uint8_t)(-e);
-  if (c.obs_fast && c.traffic_ch >= 0 && out.obs) {
-    // the tile window's traffic channel: k_env wrote it with no cars; set the car squares
-    uint8_t* o = out.obs + i * (uint64_t)c.obs_bytes + (uint64_t)c.traffic_ch * 81u;
+  if ((uint32_t)slot >= e) return;
+  const int ls = wave * cap_w + slot;  // LDS slot of the env
+  uint32_t* plan_w = lds + ls * plan_dw;
+  uint8_t* rs = reinterpret_cast<uint8_t*>(lds + (kBlock / 64) * cap_w * plan_dw + ls * rs_dw);
+  for (uint32_t r = 0; r < rounds; r++) {
+    const uint32_t j = (r * W + blockIdx.x * (kBlock / 64) + (uint32_t)wave) * e + (uint32_t)slot;
+    if (j >= n) break;
+    const uint64_t i = S.tr_list[j];
+    stage_plan(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, plan_dw);
+    Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
+    const EnvView v = rec_load(S.rec, i);
+    const int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
+    const int at = (piy / kTile) * c.tw + pix / kTile;
+    Pcg cr = stream_load(S.car, i);
+    TrafState ts{0, 0, 0, 0};
+    uint32_t CR[3] = {0u, 0u, 0u};
+    const int err = traffic_reset(c, S, i, pl, cr, rs, ts, at, CR, sub, g);
+    if (sub == 0) {
+      stream_store_state(S.car, i, cr);
+      S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.bank, 0u);
+      if (err) S.err[i] = (uint8_t)(-err);
+      if (c.obs_fast && c.traffic_ch >= 0 && out.obs) {
+        // the tile window's traffic channel: k_env wrote it with no cars; set the car squares
+        uint8_t* o = out.obs + i * (uint64_t)c.obs_bytes + (uint64_t)c.traffic_ch * 81u;
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      uint32_t m = CR[k];
-      while (m) {
-        const int b = __ffs((int)m) - 1;
-        m &= m - 1u;
-        o[k * 32 + b] = 1;
+        for (int k = 0; k < 3; k++) {
+          uint32_t m = CR[k];
+          while (m) {
+            const int b = __ffs((int)m) - 1;
+            m &= m - 1u;
+            o[k * 32 + b] = 1;
+          }
+        }
       }
     }
+    wave_lds_sync();  // the group's scratch is reused by the next round
   }
 }
 
@@ -2332,9 +2425,9 @@ struct pgtg_handle {
   size_t ev_used = 0;
   double acc_ms = 0.0;
   uint64_t acc_n = 0;
-  // k_traffic: work-list parity, lanes per workgroup and dynamic LDS
+  // k_traffic: work-list parity, grid (one workgroup per CU), envs per wave in LDS, dynamic LDS
   uint32_t tr_slot = 0;
-  int kt_lanes = 64;
+  int kt_grid = 0, kt_cap = 16;
   int kt_plan_dw = 0, kt_rs_dw = 0;
   size_t kt_lds = 0;
 };
@@ -2583,6 +2676,11 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
     c.rs_seen_off = ((2 * cap + 3) / 4) * 4;
     c.rs_pre_off = c.rs_seen_off + 4 * c.nt;
     c.rs_bytes = (c.rs_pre_off + 2 * (c.W + 1) + 3) / 4 * 4;
+    c.rs_cm_off = 0;
+    if (c.th <= 7) {  // a column's spawnable squares as one 63-bit mask: the lookup's row search is one read
+      c.rs_cm_off = c.rs_bytes;
+      c.rs_bytes += 8 * c.W;
+    }
   }
   {  // DRIVER_BEHAVIORS (pgtg/environment.py:64-109)
     const double ys[5] = {0.95, 0.75, 0.3, 0.98, 0.1}, rv[5] = {0.01, 0.05, 0.15, 0.001, 0.3};
@@ -2814,14 +2912,24 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
       // k_traffic: per-lane plan + reset scratch
       h->kt_plan_dw = odd_up((c.nt + 1) / 2);
       h->kt_rs_dw = odd_up(c.rs_bytes / 4);
-      h->kt_lanes = 64;
-      while (h->kt_lanes > 4 && (size_t)4 * h->kt_lanes * (h->kt_plan_dw + h->kt_rs_dw) + sizeof(Tables) > 150 * 1024)
-        h->kt_lanes /= 2;
-      if (const char* e = getenv("PGTG_KT_LANES")) {  // tuning knob: envs per k_traffic workgroup
-        const int want = atoi(e);
-        if (want >= 4 && want <= h->kt_lanes && (want & (want - 1)) == 0) h->kt_lanes = want;
+      // workgroups per CU (one: a second wave per SIMD measured slower than more envs per wave),
+      // then the envs per wave that fit the LDS of that many workgroups
+      const size_t per_env = (size_t)4 * (h->kt_plan_dw + h->kt_rs_dw);
+      int wpc = 1;
+      if (const char* e = getenv("PGTG_KT_WPC")) wpc = std::max(1, std::min(4, atoi(e)));  // tuning knob
+      for (;; wpc--) {
+        h->kt_cap = 32;  // envs per wave held in LDS at once
+        while (h->kt_cap > 1 && wpc * (4 * h->kt_cap * per_env + sizeof(Tables) + 256) > 160 * 1024) h->kt_cap--;
+        if (wpc == 1 || wpc * (4 * h->kt_cap * per_env + sizeof(Tables) + 256) <= 160 * 1024) break;
       }
-      h->kt_lds = (size_t)4 * h->kt_lanes * (h->kt_plan_dw + h->kt_rs_dw);
+      if (const char* e = getenv("PGTG_KT_CAP")) {  // tuning knob: envs per k_traffic wave and round
+        const int want = atoi(e);
+        if (want >= 1 && want <= h->kt_cap) h->kt_cap = want;
+      }
+      h->kt_lds = 4 * h->kt_cap * per_env;
+      int ncu = 0;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || ncu < 1) ncu = 256;
+      h->kt_grid = (int)std::min<uint64_t>((uint64_t)ncu * wpc, (h->n + 3) / 4);
       if (h->kt_lds + sizeof(Tables) > 160 * 1024) {
         g_create_err = "LDS budget exceeded (traffic reset scratch)";
         pgtg_destroy(h);
@@ -2909,9 +3017,8 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
   if (h->hcfg.need_car && mode != MODE_OBSERVE) {
     // initial traffic of the envs reset by this launch, then (windows other than the agent's tile)
     // their observation again with the cars
-    const uint64_t kb = (h->n + h->kt_lanes - 1) / h->kt_lanes;
-    hipLaunchKernelGGL(k_traffic, dim3((unsigned)kb), dim3(kBlock), h->kt_lds, h->stream, h->dcfg, h->dtab, h->S,
-                       h->out, h->tr_slot, h->kt_plan_dw, h->kt_rs_dw, h->kt_lanes);
+    hipLaunchKernelGGL(k_traffic, dim3((unsigned)h->kt_grid), dim3(kBlock), h->kt_lds, h->stream, h->dcfg, h->dtab,
+                       h->S, h->out, h->tr_slot, h->kt_plan_dw, h->kt_rs_dw, h->kt_cap);
     HIPCHK(h, hipGetLastError());
     if (!h->hcfg.obs_fast && h->hcfg.traffic_ch >= 0) {
       PgtgOutputs o{};

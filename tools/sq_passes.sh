@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counter passes (issue/stall breakdown) of one workload's step kernel.  Usage: bash tools/sq_passes.sh <tag> <workload>
+# SQ counter passes (issue/stall breakdown) of one workload's step kernel.  Usage: bash tools/sq_passes.sh <tag> <workload> [kernel substring]
 set -e
 TAG=$1; W=$2
 export TMPDIR=/tmp
@@ -12,4 +12,4 @@ for P in "$P1" "$P2"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $P -d $D/p$i -o run --output-format csv -- python bench.py --workload $W --steps 20 --warmup 5 --no-cpu-baseline > /dev/null
 done
-python tools/sq.py k_env $D/p1 $D/p2 | tail -3
+python tools/sq.py ${3:-k_env} $D/p1 $D/p2 | tail -3

@@ -22,7 +22,7 @@ PHASES = ["stage", "step", "final", "reset", "store", "obs"]
 SUB = {"cars": (16, 17), "braking": (17, 18), "reset.seed": (8, 9), "reset.generate": (9, 10),
        "reset.compile": (10, 11), "path.masks": (10, 24), "path.bfs": (24, 25), "path.walk": (25, 11), "reset.start": (11, 12), "gen.start_goal": (9, 13), "gen.edge_init": (13, 14),
        "gen.removal": (14, 15), "gen.tiles": (15, 10), "traf.spawners": (19, 20), "traf.floyd": (20, 21),
-       "traf.shuffle": (21, 22), "traf.create": (22, 23),
+       "traf.shuffle": (21, 22), "traf.lookup": (22, 26), "traf.create": (26, 23),
        "final.build": (2, 28), "final.barrier": (28, 29), "final.write": (29, 3),
        "obs.rebuild": (5, 30), "obs.barrier": (30, 31), "obs.write": (31, 6)}
 CASES = {"cfg2": (4096, dict(random_map_width=3, random_map_height=3)),
@@ -70,7 +70,8 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
         if ok.any():
             out[n] = (int((st[ok, b] - st[ok, a]).mean()), round(float(ok.mean()), 2))
     print("  sub-phases (mean cycles, fraction of waves):", out, flush=True)
-    okr = (st[:, 14] >= lo) & (st[:, 14] <= hi) & (st[:, 27] > 0) & (st[:, 27] < 1000)
+    # slot 26 is k_traffic's lookup stamp when there is traffic
+    okr = (not spread) & (st[:, 14] >= lo) & (st[:, 14] <= hi) & (st[:, 27] > 0) & (st[:, 27] < 1000)
     if okr.any():
         print("  removal loop (lane 0): iterations", round(float(st[okr, 27].mean()), 1), "max", int(st[okr, 27].max()),
               "connectivity-test cycles", int(st[okr, 26].mean()), flush=True)
