@@ -804,6 +804,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
     STAMP(26);  // (slot shared with k_env's removal-loop record: k_traffic runs later)
     if (sub != 0) return 0;
     // the cars in id order: profile and route draws
+    uint64_t a_m = cs.at(0, c.car_cap, 0);  // car slot index, advanced by the env stride
     for (int m = 0; m < k; m++) {
       const uint32_t code = out[m];
       const int x = (int)(code & 255u), y = (int)(code >> 8);
@@ -820,7 +821,8 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
       for (int j = 0; j < 4; j++) prof += (u < c.profile_t[j]) ? 0 : 1;
       const uint32_t rk = nr > 1u ? (uint32_t)pcg_draw(cr, true, nr) : 0u;
       const int route = sT.lane_route[kth_bit(rl, (int)rk)];
-      uint64_t a = cs.at(0, c.car_cap, m);
+      const uint64_t a = a_m;
+      a_m += N;
       cs.w0[a] = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
       cs.w1[a] = 0u;
       cs.id[a] = (uint32_t)m;
@@ -1191,22 +1193,21 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
   int w = 0, nnew = 0;
   // software pipeline: the next car's words are requested before the current car is processed, so
   // their HBM latency overlaps this car's work (the loop-carried copy waits only at the iteration end)
+  // slot indices advance by the env stride (no 64-bit multiply per car): the car read, the next
+  // survivor slot and the next respawn slot (respawns are written from the end backwards)
+  const uint64_t nst = S.n;
+  uint64_t ar = cs.at(cur, cap, 0), aw_i = cs.at(nxt, cap, 0), an_i = cs.at(nxt, cap, n0 - 1);
   uint32_t na, npat, nid;
-  {
-    const uint64_t ar = cs.at(cur, cap, 0);
-    na = cs.w0[ar];
-    npat = cs.w1[ar];
-    nid = cs.id[ar];
-  }
+  na = cs.w0[ar];
+  npat = cs.w1[ar];
+  nid = cs.id[ar];
   for (int r = 0; r < n0; r++) {
     const uint32_t a = na, id = nid;
     uint32_t pat = npat;
-    {
-      const uint64_t ar = cs.at(cur, cap, r + 1 < n0 ? r + 1 : r);
-      na = cs.w0[ar];
-      npat = cs.w1[ar];
-      nid = cs.id[ar];
-    }
+    if (r + 1 < n0) ar += nst;
+    na = cs.w0[ar];
+    npat = cs.w1[ar];
+    nid = cs.id[ar];
     const int x = (int)(a & 255u), y = (int)((a >> 8) & 255u), prof = (int)((a >> 21) & 7u);
     int route = (int)((a >> 16) & 31u), delay = (int)((a >> 24) & 3u);
     // ---- map lookups (no draws)
@@ -1289,7 +1290,8 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       if (nr == 0) return PGTG_E_MAP;
       const uint32_t r5 = nr > 1u ? (uint32_t)pcg_draw(cr, true, nr) : 0u;
       const int nroute = sT.lane_route[kth_bit(rl, (int)r5)];
-      const uint64_t an = cs.at(nxt, cap, n0 - 1 - nnew);
+      const uint64_t an = an_i;
+      an_i -= nst;
       cs.w0[an] = (uint32_t)sx | (uint32_t)sy << 8 | (uint32_t)nroute << 16 | (uint32_t)nprof << 21;
       cs.w1[an] = 0u;
       cs.id[an] = ts.next_id++;
@@ -1323,7 +1325,8 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
         bq.n_in++;
         hist[route]++;
       }
-      const uint64_t aw = cs.at(nxt, cap, w);
+      const uint64_t aw = aw_i;
+      aw_i += nst;
       cs.w0[aw] = (uint32_t)nx | (uint32_t)ny << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21 | (uint32_t)delay << 24;
       cs.w1[aw] = pat;
       cs.id[aw] = id;
