@@ -2933,6 +2933,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
       int ncu = 0;
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || ncu < 1) ncu = 256;
       h->kt_grid = (int)std::min<uint64_t>((uint64_t)ncu * wpc, (h->n + 3) / 4);
+      if (const char* e = getenv("PGTG_KT_GRID")) h->kt_grid = std::max(1, atoi(e));  // test knob: rounds, lane groups
       if (h->kt_lds + sizeof(Tables) > 160 * 1024) {
         g_create_err = "LDS budget exceeded (traffic reset scratch)";
         pgtg_destroy(h);

@@ -1,0 +1,73 @@
+"""k_traffic's launch shapes against the CPU oracle: the work list is levelled over the grid's waves
+(`e` envs per wave, in rounds beyond the LDS capacity `cap`) and each env gets 4, 3 or 2 lanes by `e`
+(pgtg_env.hip k_traffic / traffic_reset).  The test knobs PGTG_KT_GRID / PGTG_KT_CAP force every
+shape with small batches: quads, triples, pairs, one env per wave in many rounds."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import helpers  # noqa: F401
+from oracle.oracle import OracleEnv
+from pgtg_amd import config as cfg
+
+pytestmark = pytest.mark.gpu
+
+# (envs, grid, cap): the initial reset puts every env on the work list, so e = ceil(n / (4 * grid))
+SHAPES = {
+    "quads_e16": (512, 8, None),     # e = 16 -> 4 lanes per env
+    "triples_e20": (640, 8, None),   # e = 20 -> 3 lanes
+    "pairs_e25": (800, 8, None),     # e = 25 -> 2 lanes
+    "rounds_cap1": (96, 4, 1),       # e = 1, six rounds per wave
+    "rounds_cap5": (700, 4, 5),      # e = 5 in nine rounds of the 16 waves, 4 lanes per env
+}
+
+
+@pytest.mark.parametrize("name", sorted(SHAPES))
+def test_traffic_launch_shapes(name):
+    from pgtg_amd.vector import PGTGVecEnv
+    n, grid, cap = SHAPES[name]
+    spec = cfg.make_spec(random_map_width=5, random_map_height=5, traffic_density=0.5)
+    saved = {k: os.environ.get(k) for k in ("PGTG_KT_GRID", "PGTG_KT_CAP")}
+    os.environ["PGTG_KT_GRID"] = str(grid)
+    if cap is not None:
+        os.environ["PGTG_KT_CAP"] = str(cap)
+    try:
+        env = PGTGVecEnv(n, spec=spec, device=0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    rng = np.random.default_rng(n)
+    idx = np.unique(np.concatenate([[0, 1, 2, n // 2, n - 2, n - 1], rng.choice(n, 12, replace=False)]))
+    tix = torch.as_tensor(idx, device="cuda")
+    try:
+        env.reset(seed=11)
+        orcs = {int(i): OracleEnv(spec) for i in idx}
+        m0 = env.obs_map.index_select(0, tix).cpu().numpy()
+        for j, i in enumerate(idx):
+            r = orcs[int(i)].reset(11 + int(i))
+            assert np.array_equal(m0[j], r["obs"]), f"{name} reset obs env {int(i)}"
+            assert np.array_equal(env.cars(int(i)), orcs[int(i)].cars()), f"{name} reset cars env {int(i)}"
+        acts = env.random_actions(8, 0xBEE)
+        for t in range(8):
+            env.step_actions(acts[t])
+            torch.cuda.synchronize()
+            a = acts[t].index_select(0, tix).cpu().numpy()
+            m = env.obs_map.index_select(0, tix).cpu().numpy()
+            rew = env.reward.index_select(0, tix).cpu().numpy()
+            term = env.terminated.index_select(0, tix).cpu().numpy()
+            for j, i in enumerate(idx):
+                o = orcs[int(i)]
+                r = o.step(int(a[j]))
+                tag = f"{name} t{t} env{int(i)}"
+                assert rew[j] == r["reward"] and bool(term[j]) == r["terminated"], tag + " reward/terminated"
+                if r["terminated"]:
+                    r = o.reset(None)
+                assert np.array_equal(m[j], r["obs"]), tag + " obs"
+                assert np.array_equal(env.cars(int(i)), o.cars()), tag + " cars"
+    finally:
+        env.close()
