@@ -1,0 +1,109 @@
+"""Seeded random configurations (map size, connections, obstacles and their weights, feature lists
+in random order, sliding windows, next-subgoal direction, rewards and penalties, obstacle effect
+probabilities, traffic density, light phases, driver mix, cost channel) at multi-workgroup batch
+sizes, every step compared with the CPU oracle on a sample of envs: observations, reward, cost,
+termination, position, next-subgoal direction and cars.  The oracle is pinned to the reference's
+fixtures (tests/test_oracle_golden.py); this widens the feature combinations the HIP path is held to."""
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+import helpers  # noqa: F401
+from oracle.oracle import OracleEnv
+from pgtg_amd import config as cfg
+
+pytestmark = pytest.mark.gpu
+
+FEATURES = ["walls", "goals", "ice", "broken road", "sand", "traffic", "traffic_light", "start", "subgoal",
+            "used subgoal", "final goal", "car_spawner", "wall"]
+
+
+def random_kwargs(k: int) -> dict:
+    r = np.random.default_rng(1000 + k)
+    w, h = int(r.integers(2, 7)), int(r.integers(2, 7))
+    feats = list(r.choice(FEATURES, size=int(r.integers(1, 7)), replace=False))
+    feats += list(r.choice(cfg.LANES, size=int(r.integers(0, 3)), replace=False))
+    r.shuffle(feats)
+    prof = r.random(5) + 0.05
+    kw = dict(
+        random_map_width=w, random_map_height=h,
+        random_map_percentage_of_connections=float(r.choice([0.0, 0.3, 0.5, 0.8, 1.0])),
+        random_map_obstacle_probability=float(r.choice([0.0, 0.2, 0.6])),
+        random_map_ice_probability_weight=int(r.integers(0, 3)),
+        random_map_broken_road_probability_weight=int(r.integers(0, 3)),
+        random_map_sand_probability_weight=int(r.integers(0, 3)),
+        random_map_traffic_light_probability_weight=int(r.integers(1, 3)),
+        features_to_include_in_observation=[str(f) for f in feats],
+        use_sliding_observation_window=bool(r.random() < 0.4),
+        sliding_observation_window_size=int(r.integers(2, 6)),
+        use_next_subgoal_direction=bool(r.random() < 0.5),
+        sum_subgoals_reward=int(r.choice([0, 50, 100])),
+        final_goal_bonus=int(r.choice([0, 10])),
+        crash_penalty=int(r.choice([0, 100])),
+        traffic_light_violation_penalty=int(r.choice([0, 50])),
+        standing_still_penalty=float(r.choice([0.0, 0.5])),
+        already_visited_position_penalty=float(r.choice([0.0, 0.25])),
+        ice_probability=float(r.choice([0.0, 0.1, 0.5])),
+        street_damage_probability=float(r.choice([0.0, 0.1, 0.5])),
+        sand_probability=float(r.choice([0.0, 0.2, 0.6])),
+        traffic_density=float(r.choice([0.0, 0.0, 0.1, 0.3])) if w * h <= 25 else 0.0,
+        traffic_light_phases_duration=tuple(int(v) for v in r.integers(1, 8, size=3)),
+        ignore_traffic_collisions=bool(r.random() < 0.3),
+        separate_reward_cost=bool(r.random() < 0.5),
+    )
+    for name, p in zip(cfg.DRIVER_PROFILES, prof / prof.sum()):
+        kw[f"{name}_driver_percentage"] = float(p)
+    return kw
+
+
+@pytest.mark.parametrize("k", range(40))
+def test_random_config_parity(k):
+    from pgtg_amd.vector import PGTGVecEnv
+    kw = random_kwargs(k)
+    n, T = 768, 25
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        spec = cfg.make_spec(**kw)
+    rng = np.random.default_rng(k)
+    idx = np.unique(np.concatenate([[0, 1, 255, 256, n - 1], rng.choice(n, 9, replace=False)]))
+    tix = torch.as_tensor(idx, device="cuda")
+    env = PGTGVecEnv(n, spec=spec, device=0)
+    try:
+        env.reset(seed=100 + k)
+        orcs = {int(i): OracleEnv(spec) for i in idx}
+        m0 = env.obs_map.index_select(0, tix).cpu().numpy()
+        for j, i in enumerate(idx):
+            r = orcs[int(i)].reset(100 + k + int(i))
+            assert np.array_equal(m0[j], r["obs"]), f"case {k} reset obs env {int(i)}: {kw}"
+        acts = env.random_actions(T, 77 + k)
+        for t in range(T):
+            env.step_actions(acts[t])
+            torch.cuda.synchronize()
+            a = acts[t].index_select(0, tix).cpu().numpy()
+            m = env.obs_map.index_select(0, tix).cpu().numpy()
+            fm = env.final_map.index_select(0, tix).cpu().numpy()
+            rew = env.reward.index_select(0, tix).cpu().numpy()
+            term = env.terminated.index_select(0, tix).cpu().numpy()
+            pos = env.position.index_select(0, tix).cpu().numpy()
+            cost = env.cost.index_select(0, tix).cpu().numpy() if env.cost is not None else None
+            nsd = env.nsd.index_select(0, tix).cpu().numpy() if env.nsd is not None else None
+            for j, i in enumerate(idx):
+                o = orcs[int(i)]
+                r = o.step(int(a[j]))
+                tag = f"case {k} t{t} env{int(i)}"
+                assert rew[j] == r["reward"] and bool(term[j]) == r["terminated"], tag + f" reward/terminated {kw}"
+                if cost is not None:
+                    assert cost[j] == r["cost"], tag + " cost"
+                if r["terminated"]:
+                    assert np.array_equal(fm[j], r["obs"]), tag + " terminal obs"
+                    r = o.reset(None)
+                assert np.array_equal(m[j], r["obs"]), tag + f" obs {kw}"
+                assert tuple(pos[j]) == tuple(r["pos"]), tag + " position"
+                if nsd is not None:
+                    assert int(nsd[j]) == int(r["nsd"]), tag + " next subgoal direction"
+                if spec.traffic_density > 0:
+                    assert np.array_equal(env.cars(int(i)), o.cars()), tag + " cars"
+    finally:
+        env.close()
