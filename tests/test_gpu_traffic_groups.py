@@ -14,21 +14,25 @@ from pgtg_amd import config as cfg
 
 pytestmark = pytest.mark.gpu
 
-# (envs, grid, cap): the initial reset puts every env on the work list, so e = ceil(n / (4 * grid))
+# (envs, grid, cap, map w x h): the initial reset puts every env on the work list, so
+# e = ceil(n / (4 * grid))
 SHAPES = {
-    "quads_e16": (512, 8, None),     # e = 16 -> 4 lanes per env
-    "triples_e20": (640, 8, None),   # e = 20 -> 3 lanes
-    "pairs_e25": (800, 8, None),     # e = 25 -> 2 lanes
-    "rounds_cap1": (96, 4, 1),       # e = 1, six rounds per wave
-    "rounds_cap5": (700, 4, 5),      # e = 5 in nine rounds of the 16 waves, 4 lanes per env
+    "quads_e16": (512, 8, None, (5, 5)),     # e = 16 -> 4 lanes per env
+    "triples_e20": (640, 8, None, (5, 5)),   # e = 20 -> 3 lanes
+    "pairs_e25": (800, 8, None, (5, 5)),     # e = 25 -> 2 lanes
+    "rounds_cap1": (96, 4, 1, (5, 5)),       # e = 1, six rounds per wave
+    "rounds_cap5": (700, 4, 5, (5, 5)),      # e = 5 in nine rounds of the 16 waves, 4 lanes per env
+    # more than seven tile rows: the lookup's per-tile row search instead of the column row masks
+    "tall_map": (256, 8, None, (2, 9)),
+    "wide_map": (256, 8, None, (9, 2)),
 }
 
 
 @pytest.mark.parametrize("name", sorted(SHAPES))
 def test_traffic_launch_shapes(name):
     from pgtg_amd.vector import PGTGVecEnv
-    n, grid, cap = SHAPES[name]
-    spec = cfg.make_spec(random_map_width=5, random_map_height=5, traffic_density=0.5)
+    n, grid, cap, (mw, mh) = SHAPES[name]
+    spec = cfg.make_spec(random_map_width=mw, random_map_height=mh, traffic_density=0.5)
     saved = {k: os.environ.get(k) for k in ("PGTG_KT_GRID", "PGTG_KT_CAP")}
     os.environ["PGTG_KT_GRID"] = str(grid)
     if cap is not None:
