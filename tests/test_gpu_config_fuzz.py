@@ -1,7 +1,7 @@
 """Seeded random configurations (map size, connections, obstacles and their weights, feature lists
 in random order, sliding windows, next-subgoal direction, rewards and penalties, obstacle effect
-probabilities, traffic density, light phases, driver mix, cost channel) at multi-workgroup batch
-sizes, every step compared with the CPU oracle on a sample of envs: observations, reward, cost,
+probabilities, traffic density, light phases, driver mix, cost channel) on maps of up to 64 tiles
+and batches of 64-3000 envs, every step compared with the CPU oracle on a sample of envs: observations, reward, cost,
 termination, position, next-subgoal direction and cars.  The oracle is pinned to the reference's
 fixtures (tests/test_oracle_golden.py); this widens the feature combinations the HIP path is held to."""
 import warnings
@@ -22,7 +22,7 @@ FEATURES = ["walls", "goals", "ice", "broken road", "sand", "traffic", "traffic_
 
 def random_kwargs(k: int) -> dict:
     r = np.random.default_rng(1000 + k)
-    w, h = int(r.integers(2, 7)), int(r.integers(2, 7))
+    w, h = int(r.integers(2, 9)), int(r.integers(2, 9))  # up to 64 tiles
     feats = list(r.choice(FEATURES, size=int(r.integers(1, 7)), replace=False))
     feats += list(r.choice(cfg.LANES, size=int(r.integers(0, 3)), replace=False))
     r.shuffle(feats)
@@ -48,7 +48,7 @@ def random_kwargs(k: int) -> dict:
         ice_probability=float(r.choice([0.0, 0.1, 0.5])),
         street_damage_probability=float(r.choice([0.0, 0.1, 0.5])),
         sand_probability=float(r.choice([0.0, 0.2, 0.6])),
-        traffic_density=float(r.choice([0.0, 0.0, 0.1, 0.3])) if w * h <= 25 else 0.0,
+        traffic_density=float(r.choice([0.0, 0.0, 0.1, 0.3])) if w * h <= 30 else 0.0,
         traffic_light_phases_duration=tuple(int(v) for v in r.integers(1, 8, size=3)),
         ignore_traffic_collisions=bool(r.random() < 0.3),
         separate_reward_cost=bool(r.random() < 0.5),
@@ -62,12 +62,14 @@ def random_kwargs(k: int) -> dict:
 def test_random_config_parity(k):
     from pgtg_amd.vector import PGTGVecEnv
     kw = random_kwargs(k)
-    n, T = 768, 25
+    # batch sizes across the launch shapes (small workgroups, map queue, several workgroups)
+    n, T = int(np.random.default_rng(k).choice([64, 200, 768, 3000])), 25
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
         spec = cfg.make_spec(**kw)
     rng = np.random.default_rng(k)
-    idx = np.unique(np.concatenate([[0, 1, 255, 256, n - 1], rng.choice(n, 9, replace=False)]))
+    fixed = [i for i in (0, 1, 63, 64, 255, 256, n - 1) if i < n]
+    idx = np.unique(np.concatenate([fixed, rng.choice(n, 9, replace=False)]))
     tix = torch.as_tensor(idx, device="cuda")
     env = PGTGVecEnv(n, spec=spec, device=0)
     try:
