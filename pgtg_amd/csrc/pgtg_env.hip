@@ -661,10 +661,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 // _create_initial_traffic pgtg/environment.py:830-879), run by k_traffic for the envs k_env reset.
 // `g` (1..4) adjacent lanes of a wave share one env (`sub` 0..g-1): lane 0 runs the serial parts
 // (Floyd's choice, the shuffle, the per-car draws in id order); the sweep and the square lookup of
-// every chosen index, which have no RNG and no order, are split over the group.  `rs` is the env's LDS reset scratch:
-// Floyd's output [0, 2*cap) (then the chosen square codes), its seen set and the per-column prefix
-// of spawnable squares.  CR collects the new cars on the agent's tile `at` (observation); lane 0's
-// return value, state and CR are the result.
+// every chosen index, which have no RNG and no order, are split over the group.  `rs` is the env's
+// LDS reset scratch: Floyd's output [0, 2*cap) (then the chosen square codes), its seen set, the
+// per-column prefix of spawnable squares and (maps of <= 7 tile rows) each column's row mask.  CR
+// collects the new cars on the agent's tile `at` (observation); lane 0's return value, state and CR
+// are the result.
 __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S, uint64_t i, const Plan& pl,
                                              Pcg& cr, uint8_t* rs, TrafState& ts, int at, uint32_t* CR, int sub,
                                              int g) {
