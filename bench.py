@@ -3,12 +3,17 @@
 
 Contract (see DESIGN.md "Measurement"):
   python bench.py --gpus N --steps K --warmup W           (N>1 under torch.distributed.run)
-A "step" is one tick of every env of the rank's batch: the step kernel with same-step in-kernel
-auto-reset, reading that tick's actions (synthetic uniform policy, 1 B/env, generated on the device
-before the timed region) from HBM.  Inputs and state are resident in HBM for the whole timed region.  Each rank owns a contiguous shard of envs (global
-env g is seeded with g, weak scaling: per-GPU envs fixed); the only collectives are an RCCL
-all-reduce of the device env-step/episode counters and of the elapsed time (max).
-Prints ONE JSON line on rank 0.
+A "step" is one tick of every env of the batch: the step kernel with same-step in-kernel auto-reset,
+reading that tick's actions (synthetic uniform policy, 1 B/env, generated on the device before the
+timed region) from HBM.  Inputs and state are resident in HBM for the whole timed region.
+
+The default workload is BASELINE.json configs[4], the config its metric is quoted on: 1 048 576
+envs of 5x5 maps.  The batch is fixed and split over the ranks (strong scaling): rank r owns the
+contiguous shard of envs_total / N envs starting at global env r * envs_total / N, seeded with the
+global index and driven by the actions of the global index, so every N runs the same 1 048 576
+trajectories (bench.py --digest checks that a sharded run's outputs equal a single-GPU run's).  The
+only collectives are an RCCL all-reduce of the device env-step/episode counters and of the elapsed
+time (max).  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -22,68 +27,82 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "env-steps/sec (batched random-action rollout) at 1/2/4/8 MI355X"
-PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+PEAK_HBM_SPEC_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 WORKLOADS = {
-    # name: (BASELINE.json configs[] index, description, envs per GPU, PGTGEnv kwargs)
+    # name: (BASELINE.json configs[] index, description, envs of the whole batch, PGTGEnv kwargs)
     "cfg2": (1, "4096 vectorised envs, default 3x3 procedural map, random actions, auto-reset",
              4096, dict(random_map_width=3, random_map_height=3)),
     "cfg4": (3, "262144 envs, default 3x3 map, random actions, in-kernel auto-reset (map_generator)",
              262144, dict(random_map_width=3, random_map_height=3)),
-    "cfg5": (4, "1048576 envs sharded 8x MI355X (131072 5x5-map envs per GPU), random actions, auto-reset, "
+    "cfg5": (4, "1048576 envs of 5x5 procedural maps split over the GPUs, random actions, auto-reset, "
                 "RCCL-reduced global step counter",
-             131072, dict(random_map_width=5, random_map_height=5)),
+             1048576, dict(random_map_width=5, random_map_height=5)),
     "cfg3": (2, "65536 envs, 5x5 procedural map, traffic density 0.5, random actions, auto-reset",
              65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5)),
 }
 
 
 def algorithmic_bytes(spec, n_envs: int, resets: float, cars_per_env: float = 0.0) -> float:
-    """Bytes one step launch must move (DESIGN.md "Algorithmic bytes"): per env-step the action,
-    the 32-B agent record read+written, the 2-B/tile plan read, the observation and small outputs
-    written; per reset the seed read, the new plan written and the terminal observation written."""
+    """Bytes one step launch must move, SURVEY.md section 8(d)'s model:
+    per env-step B = 1 (action) + 2*18 (agent state r+w) + 2*H*W (tile plan r) + obs (channels x
+    window^2 int8 + 2 x 2 int32) + 10 (reward f64 + 2 flags) [+ 2*80 car_rng r+w + 2*10*C cars r+w];
+    per reset 2*H*W (plan) + 5*40 (RNG streams) + 18 (agent) + 10*C (cars) + obs (terminal obs)."""
     nt = spec.map_tiles[0] * spec.map_tiles[1]
-    obs = len(spec.channels) * spec.window ** 2
-    small = 8 + 8 + 8 + 3 + (4 if spec.next_subgoal else 0) + (8 if spec.separate_reward_cost else 0)
-    per_step = 1 + 2 * 32 + 2 * nt + obs + small
-    per_reset = 8 + 2 * nt + obs + 16 + (4 if spec.next_subgoal else 0)
+    obs = len(spec.channels) * spec.window ** 2 + 16
+    per_step = 1 + 2 * 18 + 2 * nt + obs + 10
+    per_reset = 2 * nt + 5 * 40 + 18 + obs
     if cars_per_env:
-        # cars: 12 B per car read + written per step, car_rng state 80 B r/w, traffic record 16 B r/w;
-        # resets write the new cars (12 B each) and the spawner list (2 B per spawner, ~nt)
-        per_step += 2 * 12 * cars_per_env + 2 * 40 + 2 * 16
-        per_reset += 12 * cars_per_env + 2 * nt + 80
+        per_step += 2 * 80 + 2 * 10 * cars_per_env
+        per_reset += 10 * cars_per_env
     return n_envs * per_step + resets * per_reset
 
 
-def cpu_baseline(spec, seconds: float = 12.0) -> dict:
-    """The CPU oracle (a scalar C port of the reference path; the Python reference itself cannot
-    travel to the GPU box) timed on one host core over a bounded sample of the same workload."""
+def cpu_baseline(spec, seconds: float = 15.0) -> dict:
+    """The CPU restatement (oracle/pgtg_oracle.c, a scalar C port of the reference path; the Python
+    reference itself cannot travel to the GPU box) timed on the host cores this process may use,
+    one thread per core over disjoint env ranges, on a bounded sample of the same workload."""
     from oracle import oracle
     oracle.build()
-    n_envs, steps = 64, 50
+    threads = oracle.host_threads()
+    n_envs, steps = 32 * threads, 50
     t0 = time.perf_counter()
-    done = oracle.bench(spec, n_envs, steps)
+    oracle.bench_parallel(spec, n_envs, steps, threads)
     dt = time.perf_counter() - t0
     reps = max(1, int(seconds / max(dt, 1e-3)))
     t0 = time.perf_counter()
-    done = oracle.bench(spec, n_envs * reps, steps)
+    done = oracle.bench_parallel(spec, n_envs * reps, steps, threads)
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+    return {"value": done / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "label": "restatement",
             "sample": f"{n_envs * reps} envs x {steps} random-action steps with auto-reset "
-                      f"({done} env-steps, {dt:.1f} s) on the C restatement oracle/pgtg_oracle.c"}
+                      f"({done} env-steps, {dt:.1f} s) on the C restatement oracle/pgtg_oracle.c, "
+                      f"{threads} host threads"}
 
 
-def load_traffic(workload: str, launch_bytes_alg: float):
-    """HBM bytes per step launch from the committed rocprofv3 PMC summary, if one exists."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
-    if not os.path.exists(p):
-        return None
+def measure_hbm(device: int) -> float:
+    """Measured HBM denominator: a 16-B/lane stream copy between two 2 GiB buffers (pgtg_measure_hbm),
+    (read + write) GB/s."""
+    import ctypes as C
+
+    from pgtg_amd import _abi
+    gbs = C.c_double()
+    rc = _abi.lib().pgtg_measure_hbm(device, 2 << 30, 20, C.byref(gbs))
+    return gbs.value if rc == 0 else 0.0
+
+
+def load_traffic(workload: str, n_envs: int):
+    """HBM bytes per step launch from the committed rocprofv3 PMC summary of this workload at this
+    batch size (profiles/pmc_<workload>.json, tools/pmc.py), and the file it came from."""
+    p = os.path.join("profiles", f"pmc_{workload}.json")
     try:
-        with open(p) as f:
+        with open(os.path.join(ROOT, p)) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+    except (OSError, ValueError):
+        return None, None
+    if d.get("envs") not in (None, n_envs):
+        return None, None
+    return d.get("hbm_bytes_per_launch"), p
 
 
 def main():
@@ -91,15 +110,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=50)
-    # Default: BASELINE.json's metric is quoted "at 1/2/4/8 MI355X", i.e. on configs[4] (1 048 576
-    # envs of 5x5 maps sharded over 8 GPUs); each rank runs its 131 072-env shard, so N=8 is exactly
-    # configs[4] and N=1,2,4 are its weak-scaling prefixes.  cfg2 = configs[1] (4 096 envs, one GPU).
+    # Default: configs[4] (1 048 576 envs of 5x5 maps), the config BASELINE.json's metric is quoted
+    # on, split over the N GPUs.  cfg2/cfg4/cfg3 = configs[1]/[3]/[2] (single-GPU configs).
     ap.add_argument("--workload", default="cfg5", choices=sorted(WORKLOADS))
-    ap.add_argument("--envs", type=int, default=0, help="override envs per GPU")
+    ap.add_argument("--envs", type=int, default=0, help="override the batch (envs over all GPUs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--timing-every", type=int, default=16,
                     help="bracket every n-th step launch with HIP events (kernel duration for the roofline)")
+    ap.add_argument("--digest", default="",
+                    help="after the timed window, run --digest-steps more steps and save each rank's per-env "
+                         "output digests to <path>.rank<r>.npz (tools/digest_compare.py)")
+    ap.add_argument("--digest-steps", type=int, default=8)
     args = ap.parse_args()
 
     import torch
@@ -124,17 +146,21 @@ def main():
     from pgtg_amd.dist import Shard, reduce_counters
     from pgtg_amd.vector import PGTGVecEnv
 
-    cfg_idx, desc, n_local, kwargs = WORKLOADS[args.workload]
+    cfg_idx, desc, n_total, kwargs = WORKLOADS[args.workload]
     if args.envs:
-        n_local = args.envs
+        n_total = args.envs
+    if n_total % world:
+        raise SystemExit(f"{n_total} envs do not split evenly over {world} ranks")
+    n_local = n_total // world
     spec = make_spec(**kwargs)
     shard = Shard(rank, world, n_local)
+    peak = measure_hbm(local) if rank == 0 else 0.0
     env = PGTGVecEnv(n_local, spec=spec, device=local, autoreset=True)
     env.reset(seed=shard.offset)  # global env g = rank*n_local + i gets seed g
     act_seed = 0x5EED
-    # synthetic policy: uniform actions from a counter hash of (seed, env, t), generated before the
-    # timed region so that the timed steps read their inputs from HBM like a resident rollout buffer
-    actions = env.random_actions(args.warmup + args.steps, act_seed)
+    # synthetic policy: uniform actions from a counter hash of (seed, global env, t), generated before
+    # the timed region so that the timed steps read their inputs from HBM like a resident rollout buffer
+    actions = env.random_actions(args.warmup + args.steps, act_seed, env_offset=shard.offset)
     for t in range(args.warmup):
         env.step_actions(actions[t])
     torch.cuda.synchronize(dev)
@@ -152,10 +178,26 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms, launches = env.timing_read(reset=True)
+    env.enable_timing(0)
     steps1, eps1 = env.counters()
     # RCCL (nccl backend) all-reduce: global env-step / episode counters (sum), slowest rank's time (max)
     total_steps, total_eps, t_max = reduce_counters(steps1 - steps0, eps1 - eps0, elapsed, device=red_dev)
     value = total_steps / t_max
+
+    if args.digest:
+        import numpy as np
+
+        from pgtg_amd.digest import Digest
+        del actions
+        dg = Digest(env)
+        t_end = args.warmup + args.steps
+        rows = []
+        for k in range(args.digest_steps):
+            env.step_random(act_seed, t_end + k, env_offset=shard.offset)
+            rows.append(dg.step_digest())
+        d = torch.stack(rows).cpu().numpy().view(np.uint64)
+        np.savez(f"{args.digest}.rank{rank}.npz", digest=d, offset=shard.offset, world=world,
+                 steps=t_end, workload=args.workload)
 
     if rank == 0:
         resets_per_launch = (eps1 - eps0) / max(1, args.steps)
@@ -163,20 +205,25 @@ def main():
         cars = env.mean_cars() if spec.traffic_density > 0 else 0.0
         alg = algorithmic_bytes(spec, n_local, resets_per_launch, cars)
         achieved = alg / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
+        traffic, traffic_src = load_traffic(args.workload, n_local)
         rec = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * t_max / args.steps, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int32",
-            "data": "synthetic (device uniform random actions, seeds = global env index)",
-            "config": {"workload": f"configs[{cfg_idx}]: {desc}", "envs_per_gpu": n_local,
-                       "envs_total": n_local * world, "map": f"{spec.width}x{spec.height}",
-                       "traffic_density": spec.traffic_density, "autoreset": True,
-                       "parallelism": f"dp{world} (env shards, no data-path collective)"},
+            "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+            "data": "synthetic (device uniform random actions of the global env index, seeds = global env index)",
+            "config": {"workload": f"configs[{cfg_idx}]: {desc}", "envs_total": n_total, "envs_per_gpu": n_local,
+                       "map": f"{spec.width}x{spec.height}", "traffic_density": spec.traffic_density,
+                       "autoreset": True, "parallelism": f"dp{world} (env shards, no data-path collective)"},
             "episodes": total_eps,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": load_traffic(args.workload, alg),
-                         "kernel": env.step_kernel() + " (step + in-kernel auto-reset)", "avg_kernel_us": avg_kernel_s * 1e6,
-                         "alg_bytes_per_launch": alg, "resets_per_launch": resets_per_launch,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                         "frac": achieved / peak if peak > 0 else None, "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "peak_source": "measured: pgtg_measure_hbm stream copy (2 GiB, read+write bytes)",
+                         "peak_spec": PEAK_HBM_SPEC_GBS, "frac_spec": achieved / PEAK_HBM_SPEC_GBS,
+                         "kernel": env.step_kernel() + " (step + in-kernel auto-reset)",
+                         "avg_kernel_us": avg_kernel_s * 1e6, "timed_launches": launches,
+                         "alg_bytes_per_launch": alg, "alg_model": "SURVEY.md 8(d)",
+                         "resets_per_launch": resets_per_launch, "cars_per_env": cars,
                          "envs_per_workgroup": env.launch_info()[0], "lds_bytes": env.launch_info()[1],
                          "workgroups_per_cu": env.occupancy()},
         }

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PGTG_ABI_VERSION 1
+#define PGTG_ABI_VERSION 2
 
 /* status codes (Python facade maps them to the reference's exception types) */
 #define PGTG_OK 0
@@ -110,6 +110,10 @@ typedef struct {
   int32_t autoreset;                   /* 1: same-step auto-reset (gymnasium/SB3 vector semantics) */
   int32_t max_episode_steps;           /* TimeLimit truncation, 0 = none */
   int32_t min_car_capacity;            /* car slots per env for pgtg_add_car (tests), 0 = from density */
+  /* launch-shape overrides for tests and A/B runs (0 = automatic; the library reads no environment) */
+  int32_t tune_envs_per_block;         /* 16, 32, 64, 128 or 256 env lanes per step workgroup */
+  int32_t tune_obs_sub;                /* envs per observation sub-batch */
+  int32_t tune_kt_grid, tune_kt_cap, tune_kt_wpc; /* k_traffic grid, envs per wave, workgroups per CU */
 } PgtgConfig;
 
 /* Output buffers (device pointers, caller-owned, contiguous).  NULL = not produced. */
@@ -157,8 +161,10 @@ int pgtg_reset(pgtg_handle* h, const uint64_t* seeds_host, uint64_t seed_base, c
 int pgtg_reset_unseeded(pgtg_handle* h, const uint8_t* mask_dev);
 /* One tick for every env.  actions_dev: [N] uint8 in [0, 9). */
 int pgtg_step(pgtg_handle* h, const uint8_t* actions_dev);
-/* Fill [N] uint8 actions with a counter-based uniform hash of (seed, env, t) -- synthetic rollouts. */
-int pgtg_random_actions(pgtg_handle* h, uint8_t* actions_dev, uint64_t seed, uint64_t t);
+/* Fill [N] uint8 actions with a counter-based uniform hash of (seed, env_offset + env, t) --
+ * synthetic rollouts; env_offset = global index of env 0 so that a sharded run draws the same
+ * actions as one GPU running the whole batch. */
+int pgtg_random_actions(pgtg_handle* h, uint8_t* actions_dev, uint64_t seed, uint64_t t, uint64_t env_offset);
 /* Host-synchronising introspection (copies device state). */
 int pgtg_get_env_state(pgtg_handle* h, uint64_t env, PgtgEnvState* st);
 int pgtg_get_cars(pgtg_handle* h, uint64_t env, PgtgCar* cars, int32_t cap, int32_t* n);
@@ -189,6 +195,9 @@ int pgtg_observe(pgtg_handle* h);
 int pgtg_get_counters(pgtg_handle* h, uint64_t* env_steps, uint64_t* episodes);
 /* Number of envs whose last step reported an error (PGTG_E_DONE / PGTG_E_MAP); synchronises. */
 int pgtg_error_count(pgtg_handle* h, uint64_t* n_errors, int32_t* first_code);
+/* Measured HBM denominator of the roofline: a 16-B/lane stream copy of `bytes` between two device
+ * buffers on `device`, `reps` timed passes; *copy_gbs = (read + write bytes) / s / 1e9.  Synchronises. */
+int pgtg_measure_hbm(int32_t device, uint64_t bytes, int32_t reps, double* copy_gbs);
 int pgtg_window(const pgtg_handle* h);
 uint64_t pgtg_num_envs(const pgtg_handle* h);
 /* Launch geometry of the step kernel: envs per 256-lane workgroup and dynamic LDS bytes. */

@@ -107,6 +107,8 @@ def lib():
         L.orc_choice_noreplace.argtypes = [C.POINTER(OrcPcg), C.c_int64, C.c_int64, C.POINTER(C.c_int64)]
         L.orc_bench.restype = C.c_int64
         L.orc_bench.argtypes = [C.POINTER(OrcConfig), C.c_int, C.c_int, C.c_uint64, C.c_uint64]
+        L.orc_rollout_digest.restype = C.c_int
+        L.orc_rollout_digest.argtypes = [C.POINTER(OrcConfig), C.c_int64, C.c_uint64, C.c_int, C.c_uint64, C.c_void_p]
         _lib = L
     return _lib
 
@@ -170,6 +172,63 @@ def bench(spec, n_envs: int, steps: int, seed_base: int = 0, act_seed: int = 123
     if n < 0:
         raise RuntimeError("oracle bench failed")
     return n
+
+
+def host_threads() -> int:
+    """Host cores this process may use (the GPU box's CPU share is 16, whatever os.cpu_count() says)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16
+    return max(1, min(n, cap))
+
+
+def _parallel(fn, n_envs: int, threads: int, chunk_min: int = 256):
+    """Run fn(lo, hi) over [0, n_envs) in `threads` host threads (ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    lib()
+    threads = max(1, min(threads, (n_envs + chunk_min - 1) // chunk_min))
+    bounds = [(n_envs * k // threads, n_envs * (k + 1) // threads) for k in range(threads)]
+    with ThreadPoolExecutor(threads) as ex:
+        return list(ex.map(lambda b: fn(*b), bounds))
+
+
+def rollout_digest(spec, n_envs: int, steps: int, act_seed: int, env_offset: int = 0, threads: int = 0) -> np.ndarray:
+    """[steps, n_envs] uint64 output digests of global envs env_offset..+n_envs (seed = global index,
+    actions = the GPU's splitmix hash), the formula of pgtg_amd/digest.py."""
+    c = config_from_spec(spec)
+    out = np.zeros((steps, n_envs), dtype=np.uint64)
+    # warm the library's one-time tables on this thread before fanning out
+    e = lib().orc_create(C.byref(c))
+    lib().orc_destroy(e)
+
+    def run(lo, hi):
+        if hi <= lo:
+            return 0
+        part = np.zeros((steps, hi - lo), dtype=np.uint64)
+        rc = lib().orc_rollout_digest(C.byref(c), hi - lo, env_offset + lo, steps, act_seed, part.ctypes.data)
+        if rc:
+            raise RuntimeError("oracle rollout failed")
+        out[:, lo:hi] = part
+        return hi - lo
+
+    _parallel(run, n_envs, threads or host_threads())
+    return out
+
+
+def bench_parallel(spec, n_envs: int, steps: int, threads: int, act_seed: int = 12345) -> int:
+    """orc_bench over `threads` host threads (disjoint env ranges); env-steps done."""
+    c = config_from_spec(spec)
+    e = lib().orc_create(C.byref(c))
+    lib().orc_destroy(e)
+
+    def run(lo, hi):
+        if hi <= lo:
+            return 0
+        n = lib().orc_bench(C.byref(c), hi - lo, steps, lo, act_seed)
+        if n < 0:
+            raise RuntimeError("oracle bench failed")
+        return n
+
+    return sum(_parallel(run, n_envs, threads, chunk_min=1))
 
 
 class OracleEnv:

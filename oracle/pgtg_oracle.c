@@ -1404,3 +1404,83 @@ int64_t orc_bench(const orc_config* cfg, int n_envs, int steps, uint64_t seed_ba
   free(obs);
   return done;
 }
+
+/* Per-env, per-step digests of a synthetic random-action rollout with same-step auto-reset, for the
+ * exhaustive bench-size parity tests (tests/test_gpu_exhaustive.py).  Env i of the batch is global
+ * env g = env_offset + i: seeded with g, actions from the splitmix hash of (act_seed, t, g) (the
+ * GPU's k_random_actions).  digest[t * n_envs + i] = pgtg_amd/digest.py's formula over that step's
+ * outputs: sum of W(j) over the observation's set bytes j, W(D + k) times the small outputs, and the
+ * terminal observation's bytes at W(D + 16 + j) when the env finished (all arithmetic mod 2^64). */
+static uint64_t dg_w(uint64_t j) {
+  uint64_t z = j + 1 + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static uint64_t dg_obs(const uint8_t* obs, int D, uint64_t base) {
+  uint64_t d = 0;
+  for (int j = 0; j < D; j++)
+    if (obs[j]) d += (uint64_t)obs[j] * dg_w(base + (uint64_t)j);
+  return d;
+}
+static uint64_t dg_small(const orc_out* o, int D, int nsd, int cost) {
+  uint64_t d = 0, rb, cb;
+  memcpy(&rb, &o->reward, 8);
+  memcpy(&cb, &o->cost, 8);
+  d += (uint64_t)(int64_t)o->pos[0] * dg_w(D + 0) + (uint64_t)(int64_t)o->pos[1] * dg_w(D + 1);
+  d += (uint64_t)(int64_t)o->vel[0] * dg_w(D + 2) + (uint64_t)(int64_t)o->vel[1] * dg_w(D + 3);
+  d += rb * dg_w(D + 4) + (uint64_t)(o->terminated != 0) * dg_w(D + 5) + (uint64_t)(o->truncated != 0) * dg_w(D + 6);
+  if (nsd) d += (uint64_t)(int64_t)o->next_subgoal_direction * dg_w(D + 7);
+  if (cost) d += cb * dg_w(D + 8);
+  return d;
+}
+int orc_rollout_digest(const orc_config* cfg, int64_t n_envs, uint64_t env_offset, int steps, uint64_t act_seed,
+                       uint64_t* digest) {
+  int win = cfg->sliding ? 1 + 2 * cfg->sliding_size : TILE;
+  int D = cfg->n_channels * win * win;
+  uint8_t* obs = (uint8_t*)malloc((size_t)D + 1);
+  orc_out out;
+  for (int64_t i = 0; i < n_envs; i++) {
+    const uint64_t g = env_offset + (uint64_t)i;
+    orc_env* e = orc_create(cfg);
+    if (orc_reset(e, (int64_t)g, obs, &out)) {
+      orc_destroy(e);
+      free(obs);
+      return -1;
+    }
+    for (int t = 0; t < steps; t++) {
+      uint64_t z = act_seed ^ ((uint64_t)t * 0x9E3779B97F4A7C15ull) ^ (g * 0xD1B54A32D192ED03ull);
+      z += 0x9E3779B97F4A7C15ull;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      z ^= z >> 31;
+      int a = (int)(((z >> 32) * 9ull) >> 32);
+      if (orc_step(e, a, obs, &out)) {
+        orc_destroy(e);
+        free(obs);
+        return -1;
+      }
+      uint64_t d = 0;
+      orc_out step_out = out;
+      if (out.terminated) {
+        d += dg_obs(obs, D, (uint64_t)D + 16);
+        if (orc_reset(e, -1, obs, &out)) {
+          orc_destroy(e);
+          free(obs);
+          return -1;
+        }
+        /* the vector env reports the step's reward/termination with the new episode's observation */
+        step_out.pos[0] = out.pos[0];
+        step_out.pos[1] = out.pos[1];
+        step_out.vel[0] = out.vel[0];
+        step_out.vel[1] = out.vel[1];
+        step_out.next_subgoal_direction = out.next_subgoal_direction;
+      }
+      d += dg_obs(obs, D, 0) + dg_small(&step_out, D, cfg->next_subgoal, cfg->separate_reward_cost);
+      digest[(size_t)t * (size_t)n_envs + (size_t)i] = d;
+    }
+    orc_destroy(e);
+  }
+  free(obs);
+  return 0;
+}

@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 # PGTG_LIB selects another build of the same library (test variants, pgtg_amd/build.py VARIANTS)
 LIB_PATH = os.environ.get("PGTG_LIB") or os.path.join(PKG, "libpgtg_hip.so")
 
-PGTG_ABI_VERSION = 1
+PGTG_ABI_VERSION = 2
 MAX_TILES = 64
 MAX_CHANNELS = 48
 MAX_RULES = 8
@@ -31,7 +31,7 @@ EXPORTED = [
     "pgtg_reset_unseeded", "pgtg_step", "pgtg_random_actions", "pgtg_get_env_state", "pgtg_get_cars",
     "pgtg_get_map_plan", "pgtg_get_squares", "pgtg_set_rules", "pgtg_set_agent", "pgtg_add_car", "pgtg_observe", "pgtg_get_counters",
     "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_launch_info", "pgtg_occupancy", "pgtg_step_kernel", "pgtg_last_error", "pgtg_enable_timing",
-    "pgtg_timing_read",
+    "pgtg_timing_read", "pgtg_measure_hbm",
 ]
 
 
@@ -63,6 +63,8 @@ class PgtgConfig(C.Structure):
         ("fm_exits", C.c_uint8 * MAX_TILES), ("fm_obst_type", C.c_int8 * MAX_TILES),
         ("fm_obst_mask", C.c_int8 * MAX_TILES), ("fm_start", C.c_int32 * 3), ("fm_goal", C.c_int32 * 3),
         ("autoreset", C.c_int32), ("max_episode_steps", C.c_int32), ("min_car_capacity", C.c_int32),
+        ("tune_envs_per_block", C.c_int32), ("tune_obs_sub", C.c_int32), ("tune_kt_grid", C.c_int32),
+        ("tune_kt_cap", C.c_int32), ("tune_kt_wpc", C.c_int32),
     ]
 
 
@@ -108,7 +110,8 @@ def lib():
         "pgtg_reset": ([vp, vp, u64, vp], C.c_int),
         "pgtg_reset_unseeded": ([vp, vp], C.c_int),
         "pgtg_step": ([vp, vp], C.c_int),
-        "pgtg_random_actions": ([vp, vp, u64, u64], C.c_int),
+        "pgtg_random_actions": ([vp, vp, u64, u64, u64], C.c_int),
+        "pgtg_measure_hbm": ([i32, u64, i32, C.POINTER(C.c_double)], C.c_int),
         "pgtg_get_env_state": ([vp, u64, C.POINTER(PgtgEnvState)], C.c_int),
         "pgtg_get_cars": ([vp, u64, C.POINTER(PgtgCar), i32, C.POINTER(i32)], C.c_int),
         "pgtg_get_map_plan": ([vp, u64] + [vp] * 7, C.c_int),
@@ -150,8 +153,11 @@ def fill_rules(dst, rules) -> int:
     return len(rules)
 
 
+TUNE_KEYS = ("envs_per_block", "obs_sub", "kt_grid", "kt_cap", "kt_wpc")
+
+
 def config_struct(spec: "cfgmod.EnvSpec", autoreset: bool, max_episode_steps: int | None,
-                  min_car_capacity: int = 0) -> PgtgConfig:
+                  min_car_capacity: int = 0, tune: dict | None = None) -> PgtgConfig:
     c = PgtgConfig()
     c.abi_version = PGTG_ABI_VERSION
     c.width, c.height = spec.width, spec.height
@@ -199,4 +205,8 @@ def config_struct(spec: "cfgmod.EnvSpec", autoreset: bool, max_episode_steps: in
     c.autoreset = int(autoreset)
     c.max_episode_steps = int(max_episode_steps or 0)
     c.min_car_capacity = int(min_car_capacity)
+    for k, v in (tune or {}).items():
+        if k not in TUNE_KEYS:
+            raise ValueError(f"unknown launch-shape override {k!r} (one of {TUNE_KEYS})")
+        setattr(c, "tune_" + k, int(v))
     return c

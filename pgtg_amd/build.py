@@ -18,6 +18,9 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp
 # test variant: occupancy counters saturating at 2 cars so that the exact-recount path runs often
 # (tests/test_gpu_occupancy.py replays the traffic trajectories through it)
 VARIANTS = {"occsat": ["-DPGTG_OCC_MAX=2"]}
+# A/B and diagnostic build (tools/*.sh): reads the PGTG_SPREAD/COMPACT/QUEUE/LINEMASK/DIAG knobs from
+# the environment; the product library reads none.  Not built by default (PGTG_LIB selects it).
+TOOL_VARIANTS = {"tuning": ["-DPGTG_TUNING"]}
 
 
 def variant_path(name: str) -> str:
@@ -36,7 +39,7 @@ def build(force: bool = False, verbose: bool = False, variant: str | None = None
     multi-process run can all call it: one compiles, the others wait and find it up to date."""
     import fcntl
     out = OUT if variant is None else variant_path(variant)
-    extra = [] if variant is None else VARIANTS[variant]
+    extra = [] if variant is None else {**VARIANTS, **TOOL_VARIANTS}[variant]
     with open(out + ".lock", "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
         try:

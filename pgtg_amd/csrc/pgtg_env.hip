@@ -1653,22 +1653,25 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.plan_stride_dw = odd_up((c.nt + 1) / 2);
   l.scratch_dw = c.need_car ? 0 : 3;  // with traffic: inside the (by then dead) occupancy counters
   l.traf_dw = c.need_car ? odd_up(c.traf_bytes / 4) : 0;
-  l.hist_dw = c.n_rules > 0 ? 5 : 0;
+  // route histogram of the braking rules: always with traffic (pgtg_set_rules may add rules later)
+  l.hist_dw = (c.n_rules > 0 || c.need_car) ? 5 : 0;
   l.seg_bits = c.n_channels * c.win * c.win;
   const int budget_words = 12 * 1024;  // 48 KiB observation image
   int sub = l.seg_bits > 0 ? (int)(((int64_t)budget_words - 3) * 32 / l.seg_bits) : envs;
   l.sub_envs = sub > envs ? envs : (sub < 1 ? 1 : sub);
   l.stream_words = img_words(l.sub_envs, l.seg_bits);
   l.spread = c.need_car ? 1 : 0;
-  if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);  // tuning knob
   l.compact = 1;
-  if (const char* e = getenv("PGTG_COMPACT")) l.compact = atoi(e);  // tuning knob
-  // map queue: random maps without traffic, a whole-workgroup observation image and at least one
-  // wave without env slots
-  l.queue = !c.need_car && !c.fixed_map && envs <= kBlock - 64 && l.sub_envs >= envs;
-  if (const char* e = getenv("PGTG_QUEUE")) l.queue = l.queue && atoi(e);  // tuning knob
+  // map queue: random maps without traffic or braking rules (k_envq), a whole-workgroup observation
+  // image and at least one wave without env slots
+  l.queue = !c.need_car && c.n_rules == 0 && !c.fixed_map && envs <= kBlock - 64 && l.sub_envs >= envs;
   l.diag = 0;
-  if (const char* e = getenv("PGTG_DIAG")) l.diag = atoi(e);  // diagnostic experiments only
+#ifdef PGTG_TUNING  // A/B and diagnostic builds only: the product library reads no environment
+  if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);
+  if (const char* e = getenv("PGTG_COMPACT")) l.compact = atoi(e);
+  if (const char* e = getenv("PGTG_QUEUE")) l.queue = l.queue && atoi(e);
+  if (const char* e = getenv("PGTG_DIAG")) l.diag = atoi(e);
+#endif
   lds_tail(l, c);
   return l;
 }
@@ -1682,7 +1685,9 @@ __host__ inline void lds_tail(Lds& l, const DevCfg& c) {
   const int64_t total = (int64_t)l.envs * l.seg_bits;
   const int lines = (int)((127 + total) / 128) + 1;
   l.lm_words = (!c.need_car && l.sub_envs >= l.envs && lines <= 64 * 32) ? (lines + 31) / 32 : 0;
-  if (const char* e = getenv("PGTG_LINEMASK")) l.lm_words = atoi(e) ? l.lm_words : 0;  // tuning knob
+#ifdef PGTG_TUNING
+  if (const char* e = getenv("PGTG_LINEMASK")) l.lm_words = atoi(e) ? l.lm_words : 0;
+#endif
   l.gen_off = (int)(((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
                     tail_bytes(l) / 4);
 }
@@ -2137,7 +2142,9 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
         l++;
       }
       if (l < kQueueDepth) refill(k, l);
+#ifdef PGTG_TUNING
       if (L.diag == 8 && l < kQueueDepth) refill(k, l);  // diagnostic: the same (deterministic) refill twice
+#endif
     }
     STAMP(7);
     return;
@@ -2163,7 +2170,9 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     if (lm && my_sel && out.final_obs) mark_lines(lm, out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)slot, (uint32_t)c.obs_bytes);
     ObsInfo oi;  // the post-step image of every env (terminal for the finished ones)
     build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
+#ifdef PGTG_TUNING
     if (L.diag == 9) build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);  // diagnostic
+#endif
     write_small_outputs(c, out, i, v, oi, my_sel == 1);
   }
   if (env_wave) sel[slot] = my_sel;
@@ -2385,16 +2394,32 @@ __global__ void __launch_bounds__(kBlock) k_squares(const DevCfg* __restrict__ c
   }
 }
 
-__global__ void k_random_actions(uint8_t* a, uint64_t n, uint64_t seed, uint64_t t) {
+__global__ void k_random_actions(uint8_t* a, uint64_t n, uint64_t seed, uint64_t t, uint64_t offset) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  // splitmix64 of (seed, t, i) -> Lemire multiply-shift to [0, 9)
-  uint64_t z = seed ^ (t * 0x9E3779B97F4A7C15ull) ^ (i * 0xD1B54A32D192ED03ull);
+  // splitmix64 of (seed, t, global env index) -> Lemire multiply-shift to [0, 9)
+  const uint64_t g = i + offset;
+  uint64_t z = seed ^ (t * 0x9E3779B97F4A7C15ull) ^ (g * 0xD1B54A32D192ED03ull);
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   z ^= z >> 31;
   a[i] = (uint8_t)(((z >> 32) * 9ull) >> 32);
+}
+
+// Stream copy: the measured HBM denominator of the roofline (pgtg_measure_hbm).  16 B per lane,
+// U independent loads in flight per lane, grid-stride.
+template <int U>
+__global__ void __launch_bounds__(256) k_hbm_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n16) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t b = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; b < n16; b += stride) {
+    uint4 r[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) r[j] = src[b + j * 256 < n16 ? b + j * 256 : b];
+#pragma unroll
+    for (int j = 0; j < U; j++)
+      if (b + j * 256 < n16) dst[b + j * 256] = r[j];
+  }
 }
 
 __global__ void k_fill_seeds(uint64_t* seed, uint64_t n, uint64_t base, uint64_t offset) {
@@ -2423,6 +2448,7 @@ struct pgtg_handle {
   std::vector<void*> allocs;
   std::string err;
   uint64_t seed_offset = 0;  // global index of env 0 (for sharded runs)
+  int tune_epb = 0, tune_obs_sub = 0, tune_kt_grid = 0, tune_kt_cap = 0, tune_kt_wpc = 0;  // PgtgConfig.tune_*
   int timing = 0;             // bracket every `timing`-th step launch with an event pair (0: off)
   uint64_t step_launches = 0;
   std::vector<hipEvent_t> evpool;  // pairs (start, stop) per timed launch
@@ -2732,12 +2758,109 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
 
 extern "C" {
 
+// Launch shapes of a handle from its config and batch size: envs per workgroup, the LDS layout of
+// the step kernels (observation sub-batch, map queue), k_traffic's grid and envs per wave.  Called at
+// create and again when pgtg_set_rules changes which step kernel runs.  `allow_queue`: the map
+// queue's buffers exist (or may still be allocated).  The tune_* fields of the handle (PgtgConfig,
+// 0 = automatic) force shapes for tests and A/B runs.
+static int choose_launch(pgtg_handle* h, bool allow_queue) {
+  const DevCfg& c = h->hcfg;
+  const uint64_t n_envs = h->n;
+  // envs per 256-lane workgroup.  A workgroup's time is the slowest of its lanes' serial chains, so
+  // small batches use fewer envs per workgroup to reach every CU; large batches without traffic or
+  // rules keep 128 env lanes and a helper wave that generates the next episodes' maps (k_envq, the
+  // map queue), fixed maps and rules a full workgroup of env lanes; traffic 128 (LDS).
+  const bool queue_able = allow_queue && !c.need_car && c.n_rules == 0 && !c.fixed_map;
+  int envs = c.need_car ? 128
+           : n_envs <= (uint64_t)8 * 1024 ? 16
+           : n_envs <= (uint64_t)16 * 1024 ? 32
+           : n_envs <= (uint64_t)64 * 1024 ? 64
+           : (n_envs <= (uint64_t)128 * 1024 || queue_able) ? 128 : kBlock;
+  if (h->tune_epb) envs = h->tune_epb;
+  if (envs != 16 && envs != 32 && envs != 64 && envs != 128 && envs != kBlock) envs = kBlock;
+  while (envs > 16 && lds_bytes(lds_layout(c, envs)) + sizeof(Tables) > 150 * 1024) envs /= 2;
+  h->L = lds_layout(c, envs);
+  if (c.need_car) {
+    // traffic: the most envs per workgroup (<= 128) for which two workgroups share a CU's LDS
+    // after shrinking the observation sub-batch; else the largest that fits at all
+    auto shrink = [&](Lds l) {
+      while (l.sub_envs > 8 && lds_bytes(l) + sizeof(Tables) > 80 * 1024) {
+        l.sub_envs /= 2;
+        l.stream_words = img_words(l.sub_envs, l.seg_bits);
+      }
+      return l;
+    };
+    Lds best = shrink(lds_layout(c, envs));
+    while (best.envs > 16 && lds_bytes(best) + sizeof(Tables) > 80 * 1024) best = shrink(lds_layout(c, best.envs / 2));
+    if (lds_bytes(best) + sizeof(Tables) > 80 * 1024) best = shrink(lds_layout(c, envs));
+    h->L = best;
+  }
+  if (!c.need_car && h->L.envs == kBlock) {
+    // Large batches: when the grid needs more workgroups per CU than fit the LDS (up to the 4 that
+    // the registers allow), observe in sub-batches so that the whole grid runs in one round.
+    const uint64_t blocks = (n_envs + kBlock - 1) / kBlock;
+    const int want = (int)std::min<uint64_t>(4, (blocks + 255) / 256);
+    auto fit = [&](const Lds& l) { return (int)((160 * 1024) / (lds_bytes(l) + sizeof(Tables))); };
+    while (fit(h->L) < want && h->L.sub_envs > 64) {
+      h->L.sub_envs /= 2;
+      h->L.stream_words = img_words(h->L.sub_envs, h->L.seg_bits);
+    }
+  }
+  if (h->tune_obs_sub >= 1 && h->tune_obs_sub < h->L.sub_envs) {  // forced observation sub-batch
+    h->L.sub_envs = h->tune_obs_sub;
+    h->L.stream_words = img_words(h->tune_obs_sub, h->L.seg_bits);
+  }
+  if (c.need_car) {
+    // k_traffic: per-lane plan + reset scratch
+    h->kt_plan_dw = odd_up((c.nt + 1) / 2);
+    h->kt_rs_dw = odd_up(c.rs_bytes / 4);
+    // workgroups per CU (one: a second wave per SIMD measured slower than more envs per wave),
+    // then the envs per wave that fit the LDS of that many workgroups
+    const size_t per_env = (size_t)4 * (h->kt_plan_dw + h->kt_rs_dw);
+    int wpc = h->tune_kt_wpc ? std::max(1, std::min(4, h->tune_kt_wpc)) : 1;
+    for (;; wpc--) {
+      h->kt_cap = 32;  // envs per wave held in LDS at once
+      while (h->kt_cap > 1 && wpc * (4 * h->kt_cap * per_env + sizeof(Tables) + 256) > 160 * 1024) h->kt_cap--;
+      if (wpc == 1 || wpc * (4 * h->kt_cap * per_env + sizeof(Tables) + 256) <= 160 * 1024) break;
+    }
+    if (h->tune_kt_cap >= 1 && h->tune_kt_cap <= h->kt_cap) h->kt_cap = h->tune_kt_cap;
+    h->kt_lds = 4 * h->kt_cap * per_env;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || ncu < 1) ncu = 256;
+    h->kt_grid = (int)std::min<uint64_t>((uint64_t)ncu * wpc, (h->n + 3) / 4);
+    if (h->tune_kt_grid > 0) h->kt_grid = h->tune_kt_grid;  // forced grid: rounds, lane groups
+    if (h->kt_lds + sizeof(Tables) > 160 * 1024) return fail(h, PGTG_E_UNSUPPORTED, "LDS budget exceeded (traffic reset scratch)");
+    if (h->kt_lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)k_traffic, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->kt_lds);
+  }
+  // map queue (k_envq): recheck after the adjustments above, place the helper scratch
+  h->L.queue = h->L.queue && allow_queue && h->L.sub_envs >= h->L.envs && h->L.envs <= kBlock - 64;
+  lds_tail(h->L, c);
+  if (h->L.queue && lds_bytes(h->L) + sizeof(Tables) > 40 * 1024) {  // keep 4 workgroups per CU
+    h->L.queue = 0;
+    lds_tail(h->L, c);
+  }
+  h->lds = lds_bytes(h->L);
+  if (h->lds + sizeof(Tables) > 160 * 1024) return fail(h, PGTG_E_UNSUPPORTED, "LDS budget exceeded");
+  if (h->lds > 64 * 1024) {
+    (void)hipFuncSetAttribute((const void*)k_env<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+    (void)hipFuncSetAttribute((const void*)k_env<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+    (void)hipFuncSetAttribute((const void*)k_envq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+  }
+  return PGTG_OK;
+}
+
 int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_handle** out) {
   if (!cfg || !out) return PGTG_E_INVALID;
   pgtg_handle* h = new pgtg_handle();
   *out = nullptr;
   h->device = device;
   h->n = n_envs;
+  h->tune_epb = cfg->tune_envs_per_block;
+  h->tune_obs_sub = cfg->tune_obs_sub;
+  h->tune_kt_grid = cfg->tune_kt_grid;
+  h->tune_kt_cap = cfg->tune_kt_cap;
+  h->tune_kt_wpc = cfg->tune_kt_wpc;
   int rc = 0;
   if (n_envs == 0) rc = fail(h, PGTG_E_INVALID, "n_envs must be > 0");
   if (!rc) rc = derive_cfg(h, *cfg, h->hcfg);
@@ -2863,93 +2986,10 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     pgtg_destroy(h);
     return PGTG_E_DEVICE;
   }
-  {
-    // envs per 256-lane workgroup: small batches spread over more CUs with 4 lanes per env for
-    // the observation writes; large batches keep a full workgroup of env lanes for occupancy.
-    // Traffic keeps 64 envs (one wave of car loops) per workgroup and sizes the observation
-    // sub-batch so that two workgroups share a CU's 160 KiB of LDS when the counters allow it.
-    // Small batches: fewer envs per workgroup so that every CU gets one (a workgroup's time is the
-    // slowest of its lanes' serial chains); traffic: 64 (LDS).
-    int envs = c.need_car ? 128
-             : n_envs <= (uint64_t)8 * 1024 ? 16
-             : n_envs <= (uint64_t)16 * 1024 ? 32
-             : n_envs <= (uint64_t)64 * 1024 ? 64
-             : n_envs <= (uint64_t)128 * 1024 ? 128 : kBlock;
-    if (const char* e = getenv("PGTG_ENVS_PER_BLOCK")) envs = atoi(e);
-    if (envs != 16 && envs != 32 && envs != 64 && envs != 128 && envs != kBlock) envs = kBlock;
-    while (envs > 16 && lds_bytes(lds_layout(c, envs)) + sizeof(Tables) > 150 * 1024) envs /= 2;
-    h->L = lds_layout(c, envs);
-    if (c.need_car) {
-      // traffic: the most envs per workgroup (<= 128) for which two workgroups share a CU's LDS
-      // after shrinking the observation sub-batch; else the largest that fits at all
-      auto shrink = [&](Lds l) {
-        while (l.sub_envs > 8 && lds_bytes(l) + sizeof(Tables) > 80 * 1024) {
-          l.sub_envs /= 2;
-          l.stream_words = img_words(l.sub_envs, l.seg_bits);
-        }
-        return l;
-      };
-      Lds best = shrink(lds_layout(c, envs));
-      while (best.envs > 16 && lds_bytes(best) + sizeof(Tables) > 80 * 1024) best = shrink(lds_layout(c, best.envs / 2));
-      if (lds_bytes(best) + sizeof(Tables) > 80 * 1024) best = shrink(lds_layout(c, envs));
-      h->L = best;
-    }
-    if (!c.need_car && h->L.envs == kBlock) {
-      // Large batches: when the grid needs more workgroups per CU than fit the LDS (up to the 4 that
-      // the registers allow), observe in sub-batches so that the whole grid runs in one round.
-      const uint64_t blocks = (n_envs + kBlock - 1) / kBlock;
-      const int want = (int)std::min<uint64_t>(4, (blocks + 255) / 256);
-      auto fit = [&](const Lds& l) { return (int)((160 * 1024) / (lds_bytes(l) + sizeof(Tables))); };
-      while (fit(h->L) < want && h->L.sub_envs > 64) {
-        h->L.sub_envs /= 2;
-        h->L.stream_words = img_words(h->L.sub_envs, h->L.seg_bits);
-      }
-    }
-    if (const char* e = getenv("PGTG_OBS_SUB")) {  // tuning knob: observation sub-batch size
-      int sub = atoi(e);
-      if (sub >= 1 && sub < h->L.sub_envs) {
-        h->L.sub_envs = sub;
-        h->L.stream_words = img_words(sub, h->L.seg_bits);
-      }
-    }
-    if (c.need_car) {
-      // k_traffic: per-lane plan + reset scratch
-      h->kt_plan_dw = odd_up((c.nt + 1) / 2);
-      h->kt_rs_dw = odd_up(c.rs_bytes / 4);
-      // workgroups per CU (one: a second wave per SIMD measured slower than more envs per wave),
-      // then the envs per wave that fit the LDS of that many workgroups
-      const size_t per_env = (size_t)4 * (h->kt_plan_dw + h->kt_rs_dw);
-      int wpc = 1;
-      if (const char* e = getenv("PGTG_KT_WPC")) wpc = std::max(1, std::min(4, atoi(e)));  // tuning knob
-      for (;; wpc--) {
-        h->kt_cap = 32;  // envs per wave held in LDS at once
-        while (h->kt_cap > 1 && wpc * (4 * h->kt_cap * per_env + sizeof(Tables) + 256) > 160 * 1024) h->kt_cap--;
-        if (wpc == 1 || wpc * (4 * h->kt_cap * per_env + sizeof(Tables) + 256) <= 160 * 1024) break;
-      }
-      if (const char* e = getenv("PGTG_KT_CAP")) {  // tuning knob: envs per k_traffic wave and round
-        const int want = atoi(e);
-        if (want >= 1 && want <= h->kt_cap) h->kt_cap = want;
-      }
-      h->kt_lds = 4 * h->kt_cap * per_env;
-      int ncu = 0;
-      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || ncu < 1) ncu = 256;
-      h->kt_grid = (int)std::min<uint64_t>((uint64_t)ncu * wpc, (h->n + 3) / 4);
-      if (const char* e = getenv("PGTG_KT_GRID")) h->kt_grid = std::max(1, atoi(e));  // test knob: rounds, lane groups
-      if (h->kt_lds + sizeof(Tables) > 160 * 1024) {
-        g_create_err = "LDS budget exceeded (traffic reset scratch)";
-        pgtg_destroy(h);
-        return PGTG_E_UNSUPPORTED;
-      }
-      if (h->kt_lds > 64 * 1024)
-        (void)hipFuncSetAttribute((const void*)k_traffic, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->kt_lds);
-    }
-  }
-  // map queue (k_envq): recheck after the adjustments above, place the helper scratch, allocate
-  h->L.queue = h->L.queue && h->L.sub_envs >= h->L.envs && h->L.envs <= kBlock - 64;
-  lds_tail(h->L, c);
-  if (h->L.queue && lds_bytes(h->L) + sizeof(Tables) > 40 * 1024) {  // keep 4 workgroups per CU
-    h->L.queue = 0;
-    lds_tail(h->L, c);
+  if ((rc = choose_launch(h, true))) {
+    g_create_err = h->err;
+    pgtg_destroy(h);
+    return rc;
   }
   if (h->L.queue) {
     if ((rc = dalloc(h, &h->S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw)) || (rc = dalloc(h, &h->S.qstate, n))) {
@@ -2957,18 +2997,6 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
       pgtg_destroy(h);
       return rc;
     }
-  }
-  h->lds = lds_bytes(h->L);
-  if (h->lds + sizeof(Tables) > 160 * 1024) {
-    g_create_err = "LDS budget exceeded";
-    pgtg_destroy(h);
-    return PGTG_E_UNSUPPORTED;
-  }
-  if (h->lds > 64 * 1024)
-  {
-    (void)hipFuncSetAttribute((const void*)k_env<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
-    (void)hipFuncSetAttribute((const void*)k_env<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
-    (void)hipFuncSetAttribute((const void*)k_envq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
   }
   *out = h;
   return PGTG_OK;
@@ -3069,11 +3097,11 @@ int pgtg_observe(pgtg_handle* h) {
   return launch(h, nullptr, nullptr, MODE_OBSERVE);
 }
 
-int pgtg_random_actions(pgtg_handle* h, uint8_t* actions_dev, uint64_t seed, uint64_t t) {
+int pgtg_random_actions(pgtg_handle* h, uint8_t* actions_dev, uint64_t seed, uint64_t t, uint64_t env_offset) {
   if (!h || !actions_dev) return PGTG_E_INVALID;
   HIPCHK(h, hipSetDevice(h->device));
   hipLaunchKernelGGL(k_random_actions, dim3((unsigned)((h->n + 255) / 256)), dim3(256), 0, h->stream, actions_dev, h->n,
-                     seed, t);
+                     seed, t, env_offset);
   HIPCHK(h, hipGetLastError());
   return PGTG_OK;
 }
@@ -3199,12 +3227,25 @@ int pgtg_set_rules(pgtg_handle* h, const PgtgRule* rules, int32_t n_rules) {
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   DevCfg& c = h->hcfg;
+  const DevCfg old_cfg = c;
+  const Lds old_L = h->L;
+  const size_t old_lds = h->lds;
   bool possible = c.need_car;
   for (int k = 0; k < n_rules; k++) {
     c.rules[k] = rules[k];
     possible = possible || rules[k].min_traffic <= 0;
   }
   c.n_rules = possible ? n_rules : 0;
+  if ((old_cfg.n_rules > 0) != (c.n_rules > 0)) {
+    // the step kernel changes (k_env<true> with the rules' route histogram vs k_envq / k_env<false>):
+    // lay the launch out again; the map queue only if its buffers exist
+    if (int rc = choose_launch(h, h->S.qbuf != nullptr)) {
+      c = old_cfg;
+      h->L = old_L;
+      h->lds = old_lds;
+      return rc;
+    }
+  }
   uint8_t w[PGTG_MAX_RULES][6][20] = {};
   for (int k = 0; k < n_rules; k++) memcpy(w[k], rules[k].weight, sizeof w[k]);
   HIPCHK(h, hipMemcpy(h->dcfg, &c, sizeof(DevCfg), hipMemcpyHostToDevice));
@@ -3305,6 +3346,53 @@ int pgtg_read_stamps(uint64_t* out, uint64_t n) {
 }
 #endif
 
+// The best of a few copy shapes (loads in flight per lane x workgroups per CU): the denominator is
+// what a plain stream copy reaches on this device, not the spec sheet.
+int pgtg_measure_hbm(int32_t device, uint64_t bytes, int32_t reps, double* copy_gbs) {
+  if (bytes < 16 * 1024 || reps < 1 || !copy_gbs) return PGTG_E_INVALID;
+  if (hipSetDevice(device) != hipSuccess) return PGTG_E_DEVICE;
+  const uint64_t n16 = bytes / 16;
+  void *a = nullptr, *b = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = PGTG_E_DEVICE;
+  int ncu = 256;
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+  double best = 0.0;
+  if (hipMalloc(&a, n16 * 16) == hipSuccess && hipMalloc(&b, n16 * 16) == hipSuccess &&
+      hipMemset(a, 1, n16 * 16) == hipSuccess && hipMemset(b, 2, n16 * 16) == hipSuccess &&
+      hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+    rc = PGTG_OK;
+    for (int u = 0; u < 2 && rc == PGTG_OK; u++)
+      for (int wpc = 4; wpc <= 16 && rc == PGTG_OK; wpc *= 2) {
+        const int U = u ? 8 : 4;
+        const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)ncu * wpc, (n16 + 256 * U - 1) / (256 * U));
+        auto pass = [&](int r) {
+          const uint4* src = (const uint4*)((r & 1) ? b : a);
+          uint4* dst = (uint4*)((r & 1) ? a : b);
+          if (U == 8) hipLaunchKernelGGL(k_hbm_copy<8>, dim3(grid), dim3(256), 0, 0, src, dst, n16);
+          else hipLaunchKernelGGL(k_hbm_copy<4>, dim3(grid), dim3(256), 0, 0, src, dst, n16);
+        };
+        pass(0);  // untimed: page-in, clocks
+        (void)hipEventRecord(e0, 0);
+        for (int r = 0; r < reps; r++) pass(r);
+        (void)hipEventRecord(e1, 0);
+        float ms = 0.f;
+        if (hipGetLastError() != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+            hipEventElapsedTime(&ms, e0, e1) != hipSuccess || !(ms > 0.f)) {
+          rc = PGTG_E_DEVICE;
+          break;
+        }
+        best = std::max(best, 2.0 * (double)(n16 * 16) * reps / (ms * 1e-3) / 1e9);  // read + write bytes
+      }
+  }
+  if (rc == PGTG_OK) *copy_gbs = best;
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (a) (void)hipFree(a);
+  if (b) (void)hipFree(b);
+  return rc;
+}
+
 int pgtg_window(const pgtg_handle* h) { return h ? h->hcfg.win : 0; }
 uint64_t pgtg_num_envs(const pgtg_handle* h) { return h ? h->n : 0; }
 const char* pgtg_step_kernel(const pgtg_handle* h) {
@@ -3317,7 +3405,8 @@ const char* pgtg_step_kernel(const pgtg_handle* h) {
 int pgtg_occupancy(const pgtg_handle* h, int32_t* step_blocks_per_cu) {
   if (!h) return PGTG_E_INVALID;
   int nb = 0;
-  const void* fn = h->L.queue ? (const void*)k_envq : (h->hcfg.need_car ? (const void*)k_env<true> : (const void*)k_env<false>);
+  const bool tr = h->hcfg.need_car || h->hcfg.n_rules > 0;  // the kernel launch() picks
+  const void* fn = tr ? (const void*)k_env<true> : (h->L.queue ? (const void*)k_envq : (const void*)k_env<false>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kBlock, h->lds) != hipSuccess) return PGTG_E_DEVICE;
   if (step_blocks_per_cu) *step_blocks_per_cu = nb;
   return PGTG_OK;

@@ -38,7 +38,7 @@ def _check(rc: int, handle=None) -> None:
 class PGTGVecEnv:
     def __init__(self, num_envs: int, map_path: str | None = None, *, device: int | None = None,
                  autoreset: bool = True, max_episode_steps: int | None = None, spec: EnvSpec | None = None,
-                 min_car_capacity: int = 0, **kwargs: Any):
+                 min_car_capacity: int = 0, tune: dict | None = None, **kwargs: Any):
         import torch
 
         self.spec = spec if spec is not None else make_spec(map_path, **kwargs)
@@ -49,7 +49,8 @@ class PGTGVecEnv:
             device = torch.cuda.current_device()
         self.device = torch.device("cuda", device)
         self._lib = _abi.lib()
-        self._cfg = _abi.config_struct(self.spec, autoreset, max_episode_steps, min_car_capacity)
+        # tune: launch-shape overrides for tests/A-B runs (include/pgtg.h PgtgConfig.tune_*)
+        self._cfg = _abi.config_struct(self.spec, autoreset, max_episode_steps, min_car_capacity, tune)
         h = C.c_void_p()
         _check(self._lib.pgtg_create(C.byref(self._cfg), self.num_envs, int(device), C.byref(h)), None)
         self._h = h
@@ -165,22 +166,23 @@ class PGTGVecEnv:
             infos["cost"] = self.cost
         return self.observation(), self.reward, self.terminated, self.truncated, infos
 
-    def step_random(self, seed: int, t: int):
+    def step_random(self, seed: int, t: int, env_offset: int = 0):
         """One tick with device-generated uniform random actions (synthetic rollouts, bench)."""
         self._bind_stream()
         _check(self._lib.pgtg_random_actions(self._h, C.c_void_p(self.actions.data_ptr()), C.c_uint64(seed),
-                                             C.c_uint64(t)), self._h)
+                                             C.c_uint64(t), C.c_uint64(env_offset)), self._h)
         _check(self._lib.pgtg_step(self._h, C.c_void_p(self.actions.data_ptr())), self._h)
 
-    def random_actions(self, steps: int, seed: int, t0: int = 0):
+    def random_actions(self, steps: int, seed: int, t0: int = 0, env_offset: int = 0):
         """[steps, N] uint8 device tensor of synthetic uniform actions (the same hash as step_random),
-        generated ahead so that a timed rollout starts with its inputs resident in HBM."""
+        generated ahead so that a timed rollout starts with its inputs resident in HBM.  `env_offset`
+        is the global index of env 0 (sharded runs draw the actions of the whole batch's envs)."""
         import torch
         self._bind_stream()
         a = torch.empty((steps, self.num_envs), dtype=torch.uint8, device=self.device)
         for k in range(steps):
             _check(self._lib.pgtg_random_actions(self._h, C.c_void_p(a[k].data_ptr()), C.c_uint64(seed),
-                                                 C.c_uint64(t0 + k)), self._h)
+                                                 C.c_uint64(t0 + k), C.c_uint64(env_offset)), self._h)
         return a
 
     def step_actions(self, actions_row):

@@ -1,8 +1,7 @@
 """k_traffic's launch shapes against the CPU oracle: the work list is levelled over the grid's waves
 (`e` envs per wave, in rounds beyond the LDS capacity `cap`) and each env gets 4, 3 or 2 lanes by `e`
-(pgtg_env.hip k_traffic / traffic_reset).  The test knobs PGTG_KT_GRID / PGTG_KT_CAP force every
+(pgtg_env.hip k_traffic / traffic_reset).  The launch-shape overrides tune_kt_grid / tune_kt_cap force every
 shape with small batches: quads, triples, pairs, one env per wave in many rounds."""
-import os
 
 import numpy as np
 import pytest
@@ -33,18 +32,8 @@ def test_traffic_launch_shapes(name):
     from pgtg_amd.vector import PGTGVecEnv
     n, grid, cap, (mw, mh) = SHAPES[name]
     spec = cfg.make_spec(random_map_width=mw, random_map_height=mh, traffic_density=0.5)
-    saved = {k: os.environ.get(k) for k in ("PGTG_KT_GRID", "PGTG_KT_CAP")}
-    os.environ["PGTG_KT_GRID"] = str(grid)
-    if cap is not None:
-        os.environ["PGTG_KT_CAP"] = str(cap)
-    try:
-        env = PGTGVecEnv(n, spec=spec, device=0)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    tune = {"kt_grid": grid} if cap is None else {"kt_grid": grid, "kt_cap": cap}
+    env = PGTGVecEnv(n, spec=spec, device=0, tune=tune)
     rng = np.random.default_rng(n)
     idx = np.unique(np.concatenate([[0, 1, 2, n // 2, n - 2, n - 1], rng.choice(n, 12, replace=False)]))
     tix = torch.as_tensor(idx, device="cuda")

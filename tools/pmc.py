@@ -35,7 +35,10 @@ def main():
     wl, fdir, wdir = sys.argv[1:4]
     tag = sys.argv[4] if len(sys.argv) > 4 else ""
     fetch, write = per_dispatch(fdir, "FETCH_SIZE"), per_dispatch(wdir, "WRITE_SIZE")
-    rec = {"workload": wl, "tag": tag, "unit": "bytes per step launch",
+    sys.path.insert(0, ROOT)
+    from bench import WORKLOADS
+    envs = int(os.environ.get("PGTG_PMC_ENVS", "0")) or WORKLOADS[wl][2]
+    rec = {"workload": wl, "envs": envs, "tag": tag, "unit": "bytes per step launch",
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate bench.py runs; "
                      "read bytes = 2 x FETCH_SIZE (gfx950 16-B/lane streaming-read calibration), "
                      "write bytes = WRITE_SIZE; median over the step dispatches after the first 10"}
