@@ -122,6 +122,7 @@ def main():
                     help="after the timed window, run --digest-steps more steps and save each rank's per-env "
                          "output digests to <path>.rank<r>.npz (tools/digest_compare.py)")
     ap.add_argument("--digest-steps", type=int, default=8)
+    ap.add_argument("--envs-per-block", type=int, default=0, help="A/B: force the step kernel's envs per workgroup")
     args = ap.parse_args()
 
     import torch
@@ -155,7 +156,8 @@ def main():
     spec = make_spec(**kwargs)
     shard = Shard(rank, world, n_local)
     peak = measure_hbm(local) if rank == 0 else 0.0
-    env = PGTGVecEnv(n_local, spec=spec, device=local, autoreset=True)
+    tune = {"envs_per_block": args.envs_per_block} if args.envs_per_block else None
+    env = PGTGVecEnv(n_local, spec=spec, device=local, autoreset=True, tune=tune)
     env.reset(seed=shard.offset)  # global env g = rank*n_local + i gets seed g
     act_seed = 0x5EED
     # synthetic policy: uniform actions from a counter hash of (seed, global env, t), generated before

@@ -186,6 +186,20 @@ int pgtg_get_squares(pgtg_handle* h, uint64_t env, uint64_t* words, int32_t cap,
 int pgtg_set_agent(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t vx, int32_t vy);
 /* Append a car (env.cars.append(Car(...)) in the reference tests); car_id < 0 takes the env's next id. */
 int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t route, int32_t profile, int32_t car_id);
+/* Whole-batch state for bit-exact replay: every device array that carries env state
+ * between launches (agent records, seeds, tile plans, all RNG streams with their buffered halves,
+ * visited bitsets, both car banks, traffic records, spawner lists, map queue, counters) as one host
+ * blob.  pgtg_state_size gives the blob size; pgtg_load_state accepts only a blob dumped from a handle
+ * of the same config and batch size.  Outputs are not state: call pgtg_observe after a load to
+ * re-emit the observations.  Both synchronise.  (No reference equivalent: PGTGEnv deep-copies
+ * itself in light_step, environment.py:1283-1299.) */
+int pgtg_state_size(pgtg_handle* h, uint64_t* bytes);
+int pgtg_dump_state(pgtg_handle* h, void* buf, uint64_t bytes);
+int pgtg_load_state(pgtg_handle* h, const void* buf, uint64_t bytes);
+/* PGTGEnv.set_to_state(state) (environment.py:1301-1342) for one env: position, velocity, flat tire
+ * and the car list (patience/delay 0; next car id = last id + 1 if any cars).  Synchronises. */
+int pgtg_set_to_state(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t vx, int32_t vy, int32_t flat_tire,
+                      const PgtgCar* cars, int32_t n_cars);
 /* Replace the traffic rules of every env (add_traffic_rule / remove_traffic_rule,
  * environment.py:569-575); takes effect from the next step.  n_rules <= PGTG_MAX_RULES. */
 int pgtg_set_rules(pgtg_handle* h, const PgtgRule* rules, int32_t n_rules);

@@ -90,6 +90,8 @@ def lib():
         L.orc_set_agent.argtypes = [C.c_void_p] + [C.c_int32] * 4
         L.orc_add_car.argtypes = [C.c_void_p] + [C.c_int32] * 5
         L.orc_get_squares.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_set_to_state.argtypes = [C.c_void_p] + [C.c_int32] * 5 + [C.POINTER(OrcCar), C.c_int32, C.c_void_p,
+                                                                         C.POINTER(OrcOut)]
         L.orc_last_error.restype = C.c_char_p
         L.orc_last_error.argtypes = [C.c_void_p]
         L.orc_seed_seq_state.argtypes = [C.POINTER(C.c_uint32), C.c_int, C.POINTER(C.c_uint32)]
@@ -304,6 +306,16 @@ class OracleEnv:
 
     def add_car(self, x, y, route: int, profile: int, car_id: int = -1):
         self._L.orc_add_car(self._h, int(x), int(y), int(route), int(profile), int(car_id))
+
+    def set_to_state(self, x, y, vx, vy, flat_tire, cars=()):
+        """PGTGEnv.set_to_state; cars = [(id, x, y, route, profile)]; returns the observation result."""
+        cars = list(cars)
+        arr = (OrcCar * max(1, len(cars)))()
+        for k, (cid, cx, cy, route, prof) in enumerate(cars):
+            arr[k].id, arr[k].x, arr[k].y, arr[k].route, arr[k].profile = cid, cx, cy, route, prof
+        self._L.orc_set_to_state(self._h, int(x), int(y), int(vx), int(vy), int(bool(flat_tire)), arr, len(cars),
+                                 self.obs.ctypes.data, C.byref(self.out))
+        return self.result()
 
     def squares(self) -> np.ndarray:
         n = self._L.orc_get_squares(self._h, None, 0)

@@ -1359,6 +1359,23 @@ int orc_add_car(orc_env* e, int32_t x, int32_t y, int32_t route, int32_t profile
   push_car(e, (car_t){id < 0 ? e->next_car_id++ : id, x, y, route, profile, 0, 0});
   return 0;
 }
+/* PGTGEnv.set_to_state (environment.py:1301-1342): position, velocity, flat tire; the car list is
+ * replaced by fresh Car objects (patience 0, delay 0) and _next_car_id = last id + 1 when the list is
+ * non-empty; then get_observation. */
+int orc_set_to_state(orc_env* e, int32_t x, int32_t y, int32_t vx, int32_t vy, int32_t flat_tire,
+                     const orc_car_out* cars, int32_t n_cars, uint8_t* obs, orc_out* out) {
+  e->px = x;
+  e->py = y;
+  e->vx = vx;
+  e->vy = vy;
+  e->flat_tire = flat_tire != 0;
+  e->ncars = 0;
+  for (int k = 0; k < n_cars; k++) push_car(e, (car_t){cars[k].id, cars[k].x, cars[k].y, cars[k].route, cars[k].profile, 0, 0});
+  if (n_cars > 0) e->next_car_id = cars[n_cars - 1].id + 1;
+  memset(out, 0, sizeof *out);
+  observe(e, obs, out);
+  return 0;
+}
 int orc_get_squares(const orc_env* e, uint64_t* out, int cap) {
   int n = e->W * e->H;
   for (int i = 0; i < n && i < cap; i++) out[i] = e->sq[i];

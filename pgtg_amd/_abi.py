@@ -31,7 +31,8 @@ EXPORTED = [
     "pgtg_reset_unseeded", "pgtg_step", "pgtg_random_actions", "pgtg_get_env_state", "pgtg_get_cars",
     "pgtg_get_map_plan", "pgtg_get_squares", "pgtg_set_rules", "pgtg_set_agent", "pgtg_add_car", "pgtg_observe", "pgtg_get_counters",
     "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_launch_info", "pgtg_occupancy", "pgtg_step_kernel", "pgtg_last_error", "pgtg_enable_timing",
-    "pgtg_timing_read", "pgtg_measure_hbm",
+    "pgtg_timing_read", "pgtg_measure_hbm", "pgtg_state_size", "pgtg_dump_state", "pgtg_load_state",
+    "pgtg_set_to_state",
 ]
 
 
@@ -112,6 +113,10 @@ def lib():
         "pgtg_step": ([vp, vp], C.c_int),
         "pgtg_random_actions": ([vp, vp, u64, u64, u64], C.c_int),
         "pgtg_measure_hbm": ([i32, u64, i32, C.POINTER(C.c_double)], C.c_int),
+        "pgtg_state_size": ([vp, C.POINTER(u64)], C.c_int),
+        "pgtg_dump_state": ([vp, vp, u64], C.c_int),
+        "pgtg_load_state": ([vp, vp, u64], C.c_int),
+        "pgtg_set_to_state": ([vp, u64, i32, i32, i32, i32, i32, C.POINTER(PgtgCar), i32], C.c_int),
         "pgtg_get_env_state": ([vp, u64, C.POINTER(PgtgEnvState)], C.c_int),
         "pgtg_get_cars": ([vp, u64, C.POINTER(PgtgCar), i32, C.POINTER(i32)], C.c_int),
         "pgtg_get_map_plan": ([vp, u64] + [vp] * 7, C.c_int),

@@ -242,6 +242,18 @@ class MapPlanArrays:
                 "goal": [self.goal[0], self.goal[1], DIRECTIONS[self.goal[2]]]}
 
 
+def save_map_plan(plan: dict, path: str) -> None:
+    """EpisodeMap.save_map (pgtg/map.py:173-184): a device map plan (PGTGVecEnv.map_plan) as the
+    reference's JSON (MapPlan.to_dict, pgtg/map_generator.py:31-40; '.json' appended when missing)."""
+    n = plan["w"] * plan["h"]
+    mp = MapPlanArrays(plan["w"], plan["h"], list(plan["exits"][:n]), list(plan["otype"][:n]),
+                       list(plan["omask"][:n]), tuple(plan["start"]), tuple(plan["goal"]))
+    if not path.endswith(".json"):
+        path += ".json"
+    with open(path, "w", encoding="utf-8") as f:
+        json.dump(mp.to_dict(), f, ensure_ascii=False, indent=4)
+
+
 def json_file_to_map_plan(path: str) -> MapPlanArrays:
     """pgtg/parser.py:227-241."""
     if not path.endswith(".json"):

@@ -3288,6 +3288,187 @@ int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t rou
   return PGTG_OK;
 }
 
+// ---- whole-batch state dump / load (bit-exact replay) ----------------------------------------
+// Every device array that carries an env's state from one launch to the next: agent records, seeds,
+// tile plans, error codes, counters, the four RNG streams, the visited bitsets, both car banks, the
+// traffic records, the spawner lists and the map queue.  The k_traffic work list is per-launch
+// scratch (its counters are zeroed on load).  Blob: PgtgStateHeader, n_sections x {id, pad, bytes},
+// then each section's bytes at a 16-byte aligned offset.
+namespace {
+struct StateSection {
+  uint32_t id;
+  void* ptr;
+  uint64_t bytes;
+};
+struct PgtgStateHeader {
+  char magic[4];  // "PGTS"
+  uint32_t version;
+  uint64_t n;
+  uint32_t n_sections, nt, car_cap, plan_stride;
+  uint32_t max_spawners, vis_words, qrec_dw, reserved;
+};
+struct PgtgSectionEntry {
+  uint32_t id, pad;
+  uint64_t bytes;
+};
+constexpr uint32_t kStateVersion = 1;
+}  // namespace
+
+static std::vector<StateSection> state_sections(pgtg_handle* h) {
+  const DevCfg& c = h->hcfg;
+  const DevState& S = h->S;
+  const uint64_t n = h->n;
+  std::vector<StateSection> v;
+  auto add = [&](uint32_t id, void* p, uint64_t b) {
+    if (p) v.push_back({id, p, b});
+  };
+  add(1, S.rec, n * sizeof(EnvRec));
+  add(2, S.seed, n * 8);
+  add(3, S.plan, n * (uint64_t)c.plan_stride * 2);
+  add(4, S.err, n);
+  add(5, S.counters, 16);
+  const DevStream* st[4] = {&S.car, &S.ice, &S.broken, &S.sand};
+  for (uint32_t k = 0; k < 4; k++) {
+    add(10 + 5 * k, st[k]->shi, n * 8);
+    add(11 + 5 * k, st[k]->slo, n * 8);
+    add(12 + 5 * k, st[k]->ihi, n * 8);
+    add(13 + 5 * k, st[k]->ilo, n * 8);
+    add(14 + 5 * k, st[k]->buf, n * 8);
+  }
+  add(30, S.visited, n * (uint64_t)c.vis_words * 4);
+  add(31, S.car_w0, 2 * (uint64_t)c.car_cap * n * 4);
+  add(32, S.car_w1, 2 * (uint64_t)c.car_cap * n * 4);
+  add(33, S.car_id, 2 * (uint64_t)c.car_cap * n * 4);
+  add(34, S.traf, n * sizeof(uint4));
+  add(35, S.spawners, (uint64_t)c.max_spawners * n * 2);
+  add(40, S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw * 4);
+  add(41, S.qstate, n);
+  return v;
+}
+
+static uint64_t state_blob_bytes(const std::vector<StateSection>& v) {
+  uint64_t b = sizeof(PgtgStateHeader) + v.size() * sizeof(PgtgSectionEntry);
+  for (const auto& s : v) b = ((b + 15) & ~15ull) + s.bytes;
+  return b;
+}
+
+int pgtg_state_size(pgtg_handle* h, uint64_t* bytes) {
+  if (!h || !bytes) return PGTG_E_INVALID;
+  *bytes = state_blob_bytes(state_sections(h));
+  return PGTG_OK;
+}
+
+int pgtg_dump_state(pgtg_handle* h, void* buf, uint64_t bytes) {
+  if (!h || !buf) return PGTG_E_INVALID;
+  const auto v = state_sections(h);
+  if (bytes < state_blob_bytes(v)) return fail(h, PGTG_E_INVALID, "pgtg_dump_state: buffer smaller than pgtg_state_size");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  uint8_t* p = static_cast<uint8_t*>(buf);
+  PgtgStateHeader hd{};
+  memcpy(hd.magic, "PGTS", 4);
+  hd.version = kStateVersion;
+  hd.n = h->n;
+  hd.n_sections = (uint32_t)v.size();
+  hd.nt = (uint32_t)h->hcfg.nt;
+  hd.car_cap = (uint32_t)h->hcfg.car_cap;
+  hd.plan_stride = (uint32_t)h->hcfg.plan_stride;
+  hd.max_spawners = (uint32_t)h->hcfg.max_spawners;
+  hd.vis_words = (uint32_t)h->hcfg.vis_words;
+  hd.qrec_dw = (uint32_t)h->hcfg.qrec_dw;
+  memcpy(p, &hd, sizeof hd);
+  uint64_t off = sizeof hd;
+  for (const auto& s : v) {
+    PgtgSectionEntry e{s.id, 0, s.bytes};
+    memcpy(p + off, &e, sizeof e);
+    off += sizeof e;
+  }
+  for (const auto& s : v) {
+    off = (off + 15) & ~15ull;
+    HIPCHK(h, hipMemcpy(p + off, s.ptr, s.bytes, hipMemcpyDeviceToHost));
+    off += s.bytes;
+  }
+  return PGTG_OK;
+}
+
+int pgtg_load_state(pgtg_handle* h, const void* buf, uint64_t bytes) {
+  if (!h || !buf) return PGTG_E_INVALID;
+  const auto v = state_sections(h);
+  const uint8_t* p = static_cast<const uint8_t*>(buf);
+  PgtgStateHeader hd;
+  if (bytes < sizeof hd) return fail(h, PGTG_E_INVALID, "pgtg_load_state: truncated state");
+  memcpy(&hd, p, sizeof hd);
+  if (memcmp(hd.magic, "PGTS", 4) != 0 || hd.version != kStateVersion)
+    return fail(h, PGTG_E_INVALID, "pgtg_load_state: not a state blob of this version");
+  if (hd.n != h->n || hd.n_sections != v.size() || hd.nt != (uint32_t)h->hcfg.nt ||
+      hd.car_cap != (uint32_t)h->hcfg.car_cap || hd.plan_stride != (uint32_t)h->hcfg.plan_stride ||
+      hd.max_spawners != (uint32_t)h->hcfg.max_spawners || hd.vis_words != (uint32_t)h->hcfg.vis_words ||
+      hd.qrec_dw != (uint32_t)h->hcfg.qrec_dw || bytes < state_blob_bytes(v))
+    return fail(h, PGTG_E_INVALID, "pgtg_load_state: the state was dumped from a handle of another shape");
+  uint64_t off = sizeof hd;
+  for (const auto& s : v) {
+    PgtgSectionEntry e;
+    memcpy(&e, p + off, sizeof e);
+    off += sizeof e;
+    if (e.id != s.id || e.bytes != s.bytes) return fail(h, PGTG_E_INVALID, "pgtg_load_state: section table mismatch");
+  }
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (const auto& s : v) {
+    off = (off + 15) & ~15ull;
+    HIPCHK(h, hipMemcpy(s.ptr, p + off, s.bytes, hipMemcpyHostToDevice));
+    off += s.bytes;
+  }
+  if (h->S.tr_count) HIPCHK(h, hipMemset(h->S.tr_count, 0, 2 * sizeof(uint32_t)));
+  return PGTG_OK;
+}
+
+// PGTGEnv.set_to_state (environment.py:1301-1342) for env `env`: position, velocity and flat tire,
+// then the car list replaced by `cars` (patience and delay 0, like the reference's fresh Car
+// objects); the next car id becomes the last car's id + 1 when the list is non-empty.  Map, RNG
+// streams, termination and subgoals are untouched.  n_cars <= 0: no cars.
+int pgtg_set_to_state(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t vx, int32_t vy, int32_t flat_tire,
+                      const PgtgCar* cars, int32_t n_cars) {
+  if (!h || env >= h->n || (n_cars > 0 && !cars)) return PGTG_E_INVALID;
+  if (abs(vx) > 30000 || abs(vy) > 30000 || abs(x) > 30000 || abs(y) > 30000)
+    return fail(h, PGTG_E_UNSUPPORTED, "position/velocity outside the 16-bit state range");
+  const DevCfg& c = h->hcfg;
+  if (n_cars > 0 && !c.need_car) return fail(h, PGTG_E_UNSUPPORTED, "create the handle with min_car_capacity > 0 or traffic");
+  if (n_cars > c.car_cap) return fail(h, PGTG_E_UNSUPPORTED, "more cars than the handle's car capacity");
+  for (int k = 0; k < n_cars; k++) {
+    const PgtgCar& q = cars[k];
+    if (q.x < 0 || q.y < 0 || q.x >= c.W || q.y >= c.H || q.route < 0 || q.route >= 20 || q.profile < 0 || q.profile >= 5)
+      return fail(h, PGTG_E_INVALID, "car outside the map or bad route/profile");
+  }
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  EnvRec r;
+  HIPCHK(h, hipMemcpy(&r, h->S.rec + env, sizeof r, hipMemcpyDeviceToHost));
+  r.a.x = ((uint32_t)x & 0xffffu) | ((uint32_t)y << 16);
+  r.a.y = ((uint32_t)vx & 0xffffu) | ((uint32_t)vy << 16);
+  uint32_t flags = (r.a.z >> 16) & 0xffu;
+  flags = flat_tire ? (flags | kFlagFlatTire) : (flags & ~kFlagFlatTire);
+  r.a.z = (r.a.z & 0xff00ffffu) | (flags << 16);
+  HIPCHK(h, hipMemcpy(h->S.rec + env, &r, sizeof r, hipMemcpyHostToDevice));
+  if (c.need_car) {
+    uint4 t;
+    if (int rc = read_traf(h, env, &t)) return rc;
+    const int bank = (int)t.z, nc = n_cars > 0 ? n_cars : 0;
+    for (int k = 0; k < nc; k++) {
+      const uint64_t a = ((uint64_t)bank * c.car_cap + k) * h->n + env;
+      const uint32_t w0 = (uint32_t)cars[k].x | (uint32_t)cars[k].y << 8 | (uint32_t)cars[k].route << 16 |
+                          (uint32_t)cars[k].profile << 21, w1 = 0, id = (uint32_t)cars[k].id;
+      HIPCHK(h, hipMemcpy(h->S.car_w0 + a, &w0, 4, hipMemcpyHostToDevice));
+      HIPCHK(h, hipMemcpy(h->S.car_w1 + a, &w1, 4, hipMemcpyHostToDevice));
+      HIPCHK(h, hipMemcpy(h->S.car_id + a, &id, 4, hipMemcpyHostToDevice));
+    }
+    t.x = (t.x & 0xffff0000u) | (uint32_t)nc;
+    if (nc > 0) t.y = (uint32_t)cars[nc - 1].id + 1u;
+    HIPCHK(h, hipMemcpy(h->S.traf + env, &t, sizeof t, hipMemcpyHostToDevice));
+  }
+  return PGTG_OK;
+}
+
 int pgtg_get_counters(pgtg_handle* h, uint64_t* env_steps, uint64_t* episodes) {
   if (!h) return PGTG_E_INVALID;
   HIPCHK(h, hipSetDevice(h->device));

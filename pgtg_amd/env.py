@@ -200,6 +200,37 @@ class PGTGEnv:
     def close(self):
         self._vec.close()
 
+    def light_step(self, action: int):
+        """environment.py:1283-1299: a step on a copy; this env is unchanged afterwards.  The copy is
+        the device state blob (pgtg_dump_state / pgtg_load_state), so RNG streams are restored too."""
+        blob = self._vec.dump_state()
+        flags = (self.terminated, self.truncated, self._triggered)
+        try:
+            out = self.step(action)
+        finally:
+            self._vec.load_state(blob)
+            self.terminated, self.truncated, self._triggered = flags
+        return out
+
+    def set_to_state(self, state: dict[str, Any]):
+        """environment.py:1301-1342: position, velocity, flat tire and the car list (patience and delay
+        reset, unknown driver profiles -> normal, next car id = last id + 1); returns (obs, info)."""
+        cars = []
+        for cd in state.get("cars") or []:
+            prof = cd.get("driver_profile", "normal")
+            if prof not in _cfg.DRIVER_PROFILES:
+                prof = "normal"
+            cars.append((int(cd["id"]), int(cd["x"]), int(cd["y"]), _cfg.ROUTES.index(cd["route"]),
+                         _cfg.DRIVER_PROFILES.index(prof)))
+        self._vec.set_to_state(0, int(state["x"]), int(state["y"]), int(state["x_velocity"]),
+                               int(state["y_velocity"]), bool(state["flat_tire"]), cars)
+        self._vec.observe()
+        return self.get_observation(), self.get_info()
+
+    def save_map(self, path: str) -> None:
+        """pgtg/map.py:173-184: the episode's map plan as JSON (loadable with map_path=)."""
+        _cfg.save_map_plan(self._vec.map_plan(0), path)
+
     def render(self):
         return None
 

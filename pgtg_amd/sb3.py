@@ -47,7 +47,10 @@ class PGTGSB3VecEnv:
         return flatten_obs(self.spec, obs).cpu().numpy()
 
     def step_async(self, actions) -> None:
-        self._actions = np.asarray(actions, dtype=np.uint8).reshape(self.num_envs)
+        a = np.asarray(actions).reshape(self.num_envs)
+        if a.size and (a.min() < 0 or a.max() > 8):  # an out-of-space action raises (environment.py:1118)
+            raise KeyError(int(a[(a < 0) | (a > 8)][0]))
+        self._actions = a.astype(np.uint8)
 
     def step_wait(self):
         import torch

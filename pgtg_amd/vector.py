@@ -139,7 +139,12 @@ class PGTGVecEnv:
                 raise ValueError("seed must be a non-negative int")
             _check(self._lib.pgtg_reset(self._h, None, C.c_uint64(seed), mptr), self._h)
         else:
-            seeds = (C.c_uint64 * self.num_envs)(*[int(s) for s in seed])
+            seeds_l = [int(s) for s in seed]
+            if len(seeds_l) != self.num_envs:
+                raise ValueError(f"reset(seed=list) needs {self.num_envs} seeds, got {len(seeds_l)}")
+            if any(s < 0 for s in seeds_l):
+                raise ValueError("seed must be a non-negative int")
+            seeds = (C.c_uint64 * self.num_envs)(*seeds_l)
             _check(self._lib.pgtg_reset(self._h, seeds, 0, mptr), self._h)
         self._seeded = True
         return self.observation(), {}
@@ -148,7 +153,17 @@ class PGTGVecEnv:
         import torch
         self._bind_stream()
         if not isinstance(actions, torch.Tensor):
-            actions = torch.as_tensor(actions)
+            import numpy as np
+            host = np.asarray(actions)
+            if host.shape != (self.num_envs,):
+                raise ValueError(f"expected {self.num_envs} actions, got shape {host.shape}")
+            if host.size and (host.min() < 0 or host.max() > 8):  # Discrete(9): environment.py:1118
+                raise KeyError(int(host[(host < 0) | (host > 8)][0]))
+            actions = torch.as_tensor(host.astype(np.uint8))
+        elif actions.numel() != self.num_envs:
+            raise ValueError(f"expected {self.num_envs} actions, got {actions.numel()}")
+        elif bool(((actions < 0) | (actions > 8)).any()):  # one device sync; step_actions() skips it
+            raise KeyError("action outside Discrete(9)")
         a = actions
         if a.device != self.device or a.dtype != torch.uint8:
             a = a.to(device=self.device, dtype=torch.uint8)
@@ -262,6 +277,35 @@ class PGTGVecEnv:
 
     def rule_names(self) -> list[str]:
         return [r.name for r in self.spec.rules]
+
+    # -- whole-batch state (bit-exact replay) and set_to_state --------------------------------------
+    def dump_state(self):
+        """Every env's device state as one uint8 numpy blob (include/pgtg.h pgtg_dump_state)."""
+        import numpy as np
+        n = C.c_uint64()
+        _check(self._lib.pgtg_state_size(self._h, C.byref(n)), self._h)
+        buf = np.empty(n.value, dtype=np.uint8)
+        _check(self._lib.pgtg_dump_state(self._h, C.c_void_p(buf.ctypes.data), n.value), self._h)
+        return buf
+
+    def load_state(self, blob, observe: bool = True):
+        """Restore a dump_state() blob of a handle with the same config and batch size; re-emits the
+        observations unless observe=False."""
+        import numpy as np
+        b = np.ascontiguousarray(blob, dtype=np.uint8)
+        _check(self._lib.pgtg_load_state(self._h, C.c_void_p(b.ctypes.data), b.size), self._h)
+        self._seeded = True
+        if observe:
+            self.observe()
+
+    def set_to_state(self, i: int, x: int, y: int, vx: int, vy: int, flat_tire: bool, cars=()):
+        """PGTGEnv.set_to_state for env i (environment.py:1301-1342); cars = [(id, x, y, route, profile)]."""
+        cars = list(cars)
+        arr = (_abi.PgtgCar * max(1, len(cars)))()
+        for k, (cid, cx, cy, route, prof) in enumerate(cars):
+            arr[k].id, arr[k].x, arr[k].y, arr[k].route, arr[k].profile = int(cid), int(cx), int(cy), int(route), int(prof)
+        _check(self._lib.pgtg_set_to_state(self._h, i, int(x), int(y), int(vx), int(vy), int(bool(flat_tire)), arr,
+                                           len(cars)), self._h)
 
     def set_agent(self, i: int, x: int, y: int, vx: int, vy: int):
         _check(self._lib.pgtg_set_agent(self._h, i, x, y, vx, vy), self._h)
