@@ -180,3 +180,75 @@ def test_triggered_mask_over_golden_braking_trajectory():
             done[i] = bool(term[i])
     assert hits > 0
     vec.close()
+
+
+def _vec_vs_oracle(vec, spec_orc, n, steps, seed, rng, tag):
+    """Autoreset batch vs per-env oracles: reward, termination, observation and braking mask."""
+    import torch
+    orcs = [OracleEnv(spec_orc) for _ in range(n)]
+    for i, o in enumerate(orcs):
+        o.reset(seed + i)
+    fired = 0
+    for t in range(steps):
+        acts = rng.integers(0, 9, n).astype(np.uint8)
+        vec.step(torch.as_tensor(acts))
+        torch.cuda.synchronize()
+        m, rew = vec.obs_map.cpu().numpy(), vec.reward.cpu().numpy()
+        term, mask = vec.terminated.cpu().numpy(), vec.braking.cpu().numpy()
+        for i, o in enumerate(orcs):
+            r = o.step(int(acts[i]))
+            assert rew[i] == r["reward"] and bool(term[i]) == r["terminated"], f"{tag} t{t} env{i}"
+            assert int(mask[i]) == int(r["braking"]), f"{tag} t{t} env{i} braking"
+            fired += int(mask[i] != 0)
+            if r["terminated"]:
+                r = o.reset(None)
+            assert np.array_equal(m[i], r["obs"]), f"{tag} t{t} env{i} obs"
+    return fired
+
+
+def test_rules_added_to_a_ruleless_traffic_handle():
+    """A traffic handle created without rules, then add_traffic_rule (environment.py:569-575): the
+    braking pass must use its own per-lane route histogram (layout reserved with traffic)."""
+    from pgtg_amd.vector import PGTGVecEnv
+    full = _spec(random_map_width=5, random_map_height=5, traffic_density=0.5)
+    bare = copy.deepcopy(full)
+    bare.rules = []
+    vec = PGTGVecEnv(64, spec=bare, device=0)
+    try:
+        vec.reset(seed=300)
+        for r in cfg.DEFAULT_RULES:
+            vec.add_traffic_rule(r)
+        fired = _vec_vs_oracle(vec, full, 64, 25, 300, np.random.default_rng(5), "traffic+rules")
+        assert fired > 0
+    finally:
+        vec.close()
+
+
+def test_zero_traffic_rule_on_a_handle_without_traffic():
+    """A rule with min_traffic = 0 fires without cars: adding it to a no-traffic handle switches the
+    step kernel (k_envq -> k_env<true> with the rules' histogram), removing it switches back."""
+    from pgtg_amd.vector import PGTGVecEnv
+    rule = {"name": "brake_on_crossings", "tile_type": "1111", "velocity_range": [0.5, 10.0], "min_traffic": 0,
+            "min_matching_traffic": 0,
+            "maneuvers": [{"agent": d, "traffic": ["north_to_south"]} for d in
+                          ("west_to_east", "east_to_west", "north_to_south", "south_to_north", "near_goal")]}
+    base = _spec(random_map_width=4, random_map_height=4)
+    base.rules = []
+    with_rule = copy.deepcopy(base)
+    cfg.add_rule(with_rule, rule)
+    vec = PGTGVecEnv(48, spec=copy.deepcopy(base), device=0)
+    try:
+        assert vec.step_kernel() == "pgtg::k_envq"
+        vec.reset(seed=70)
+        vec.add_traffic_rule(rule)
+        assert vec.step_kernel() == "pgtg::k_env<true>"
+        rng = np.random.default_rng(6)
+        fired = _vec_vs_oracle(vec, with_rule, 48, 30, 70, rng, "rule")
+        assert fired > 0
+        # back without the rule: the state carries on; compare from a fresh seeded reset
+        assert vec.remove_traffic_rule("brake_on_crossings")
+        assert vec.step_kernel() == "pgtg::k_envq"
+        vec.reset(seed=900)
+        _vec_vs_oracle(vec, base, 48, 20, 900, rng, "no rule")
+    finally:
+        vec.close()

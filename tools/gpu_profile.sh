@@ -8,7 +8,7 @@ shift || true
 WLS=${@:-cfg2 cfg4 cfg5 cfg3}
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof_$TAG
-python -c "from pgtg_amd.build import build; build()"
+python -c "from pgtg_amd.build import build; build()" || exit 1
 for W in $WLS; do
   D=gpurun_out/prof_$TAG/$W
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/trace -o run --output-format csv -- python bench.py --workload $W --steps 100 --warmup 20 --no-cpu-baseline > $D.trace.json
