@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PGTG_ABI_VERSION 2
+#define PGTG_ABI_VERSION 3
 
 /* status codes (Python facade maps them to the reference's exception types) */
 #define PGTG_OK 0
@@ -114,6 +114,7 @@ typedef struct {
   int32_t tune_envs_per_block;         /* 16, 32, 64, 128 or 256 env lanes per step workgroup */
   int32_t tune_obs_sub;                /* envs per observation sub-batch */
   int32_t tune_kt_grid, tune_kt_cap, tune_kt_wpc; /* k_traffic grid, envs per wave, workgroups per CU */
+  int32_t tune_car_slots;              /* car slots per env (>= 3 x capacity + 4; tests of the bound) */
 } PgtgConfig;
 
 /* Output buffers (device pointers, caller-owned, contiguous).  NULL = not produced. */
@@ -140,7 +141,7 @@ typedef struct {
   int32_t n_cars, next_car_id, path_len, error;
   uint32_t spawn_counter;
   uint64_t seed, used_subgoals;
-  int32_t n_spawners, reserved;
+  int32_t n_spawners, car_tail;        /* car slots in use (cars + empty slots before the last car) */
 } PgtgEnvState;
 
 typedef struct {

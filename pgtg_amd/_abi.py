@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 # PGTG_LIB selects another build of the same library (test variants, pgtg_amd/build.py VARIANTS)
 LIB_PATH = os.environ.get("PGTG_LIB") or os.path.join(PKG, "libpgtg_hip.so")
 
-PGTG_ABI_VERSION = 2
+PGTG_ABI_VERSION = 3
 MAX_TILES = 64
 MAX_CHANNELS = 48
 MAX_RULES = 8
@@ -65,7 +65,7 @@ class PgtgConfig(C.Structure):
         ("fm_obst_mask", C.c_int8 * MAX_TILES), ("fm_start", C.c_int32 * 3), ("fm_goal", C.c_int32 * 3),
         ("autoreset", C.c_int32), ("max_episode_steps", C.c_int32), ("min_car_capacity", C.c_int32),
         ("tune_envs_per_block", C.c_int32), ("tune_obs_sub", C.c_int32), ("tune_kt_grid", C.c_int32),
-        ("tune_kt_cap", C.c_int32), ("tune_kt_wpc", C.c_int32),
+        ("tune_kt_cap", C.c_int32), ("tune_kt_wpc", C.c_int32), ("tune_car_slots", C.c_int32),
     ]
 
 
@@ -79,7 +79,7 @@ class PgtgEnvState(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("x", "y", "vx", "vy", "terminated", "flat_tire", "phase", "elapsed",
                                          "n_cars", "next_car_id", "path_len", "error")] + [
         ("spawn_counter", C.c_uint32), ("seed", C.c_uint64), ("used_subgoals", C.c_uint64),
-        ("n_spawners", C.c_int32), ("reserved", C.c_int32)]
+        ("n_spawners", C.c_int32), ("car_tail", C.c_int32)]
 
 
 class PgtgCar(C.Structure):
@@ -158,7 +158,7 @@ def fill_rules(dst, rules) -> int:
     return len(rules)
 
 
-TUNE_KEYS = ("envs_per_block", "obs_sub", "kt_grid", "kt_cap", "kt_wpc")
+TUNE_KEYS = ("envs_per_block", "obs_sub", "kt_grid", "kt_cap", "kt_wpc", "car_slots")
 
 
 def config_struct(spec: "cfgmod.EnvSpec", autoreset: bool, max_episode_steps: int | None,

@@ -67,7 +67,8 @@ struct DevCfg {
   int32_t need_car, need_ice, need_broken, need_sand;
   double density;
   uint64_t profile_t[5];  // profile CDF as 53-bit thresholds: random() < cdf[j]  <=>  (next64 >> 11) < t[j]
-  int32_t car_cap;      // car slots per env and bank
+  int32_t car_cap;      // cars an env can hold (initial traffic <= this; pgtg_add_car / set_to_state limit)
+  int32_t car_slots;    // car slots per env (>= 2 * car_cap: empty slots + a tick of respawns)
   int32_t max_spawners; // spawner list capacity per env (nt * 5)
   // DRIVER_BEHAVIORS (pgtg/environment.py:64-109) in DriverProfile order, thresholds precomputed
   // random() < p  <=>  (next64 >> 11) < ceil(p * 2^53): probabilities as integer thresholds
@@ -140,9 +141,12 @@ struct DevState {
   uint16_t* plan;         // [n][plan_stride]
   DevStream car, ice, broken, sand;
   uint32_t* visited;      // [n][vis_words] or null
-  // traffic: two banks of car slots, car-major / env-minor ([bank][slot][n]) so that the lanes of a
-  // wave read slot k of 64 envs with one coalesced access.  w0 = x | y<<8 | route<<16 | profile<<21 |
-  // delay<<24, w1 = patience counter, id = car id.  traf[n] = {n_cars | n_spawners<<16, next_id, bank, 0}
+  // traffic: one bank of car slots per env in id order (= the reference's list order), slot-major /
+  // env-minor ([slots][n]) so that the lanes of a wave read or write slot k of their envs with one
+  // coalesced access.  w0 = x | y<<8 | route<<16 | profile<<21 | delay<<24 (bit 31: empty slot, a
+  // despawned car), w1 = patience counter, id = car id.  Survivors are rewritten in place, respawns
+  // appended behind the tail, the slots compacted when a tick's respawns could overrun them.
+  // traf[n] = {n_cars | n_spawners<<16, next_id, tail (slots in use), 0}
   uint32_t* car_w0;
   uint32_t* car_w1;
   uint32_t* car_id;

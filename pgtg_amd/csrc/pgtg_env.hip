@@ -244,7 +244,7 @@ __device__ __forceinline__ bool square_tlight(const DevCfg& c, const Plan& pl, i
 }
 // Occupancy counters are 4-bit (two lane slots per byte, 16 B per tile) so that 256 envs' counters
 // fit a CU's LDS.  A counter saturates at kOccMax and raises the lane's `sat` flag; decrementing a
-// saturated counter then recounts that square exactly from the car banks (rare: squares with 15
+// saturated counter then recounts that square exactly from the car slots (rare: squares with 15
 // cars), so every count the dynamics see is exact.  Test builds lower kOccMax to exercise it.
 #ifndef PGTG_OCC_MAX
 #define PGTG_OCC_MAX 15
@@ -270,11 +270,12 @@ __device__ __forceinline__ int kth_bit(uint32_t m, int k) {
   return __ffs((int)m) - 1;
 }
 
-struct CarStore {  // one env's view of the car banks
+constexpr uint32_t kCarEmpty = 1u << 31;  // w0 of a slot without a car
+struct CarSlots {  // one env's car slots (DevState::car_w0 layout): slot k of env i at k * n + i
   uint32_t *w0, *w1, *id;
   uint64_t n;  // stride between slots (= number of envs)
   uint64_t i;  // env index
-  __device__ __forceinline__ uint64_t at(int bank, int cap, int k) const { return ((uint64_t)bank * cap + k) * n + i; }
+  __device__ __forceinline__ uint64_t at(int k) const { return (uint64_t)k * n + i; }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -634,7 +635,7 @@ __device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, int
 }
 
 struct TrafState {
-  uint32_t n_cars, n_spawners, next_id, bank;
+  uint32_t n_cars, n_spawners, next_id, tail;  // tail: car slots in use (cars and empty slots)
 };
 
 // spawner squares of local column lx of tile (tx, ty): lane-data spawners (dead ends) plus the
@@ -723,7 +724,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
   wave_lds_sync();
   const int ncars = (int)((double)np * c.density);  // int(len(positions) * traffic_density)
   int k = 0;
-  CarStore cs{S.car_w0, S.car_w1, S.car_id, N, i};
+  const CarSlots cs{S.car_w0, S.car_w1, S.car_id, N, i};
   if (ncars > 0 && np > 0) {
     k = min(ncars, np);
     if (k > c.car_cap) return PGTG_E_UNSUPPORTED;
@@ -804,8 +805,8 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
     wave_lds_sync();
     STAMP(26);  // (slot shared with k_env's removal-loop record: k_traffic runs later)
     if (sub != 0) return 0;
-    // the cars in id order: profile and route draws
-    uint64_t a_m = cs.at(0, c.car_cap, 0);  // car slot index, advanced by the env stride
+    // the cars in id order: profile and route draws -> slots 0 .. k-1
+    uint64_t a_m = cs.at(0);  // slot index, advanced by the env stride
     for (int m = 0; m < k; m++) {
       const uint32_t code = out[m];
       const int x = (int)(code & 255u), y = (int)(code >> 8);
@@ -822,18 +823,17 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
       for (int j = 0; j < 4; j++) prof += (u < c.profile_t[j]) ? 0 : 1;
       const uint32_t rk = nr > 1u ? (uint32_t)pcg_draw(cr, true, nr) : 0u;
       const int route = sT.lane_route[kth_bit(rl, (int)rk)];
-      const uint64_t a = a_m;
+      cs.w0[a_m] = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
+      cs.w1[a_m] = 0u;
+      cs.id[a_m] = (uint32_t)m;
       a_m += N;
-      cs.w0[a] = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
-      cs.w1[a] = 0u;
-      cs.id[a] = (uint32_t)m;
     }
   }
   STAMP(23);
   ts.n_cars = (uint32_t)k;
   ts.n_spawners = (uint32_t)min(nsp, c.max_spawners);
   ts.next_id = (uint32_t)k;
-  ts.bank = 0;
+  ts.tail = (uint32_t)k;
   return 0;
 }
 
@@ -1153,8 +1153,9 @@ struct BrakeQuery {
 };
 // Traffic tick: every car of the tick-start list, in list order (pgtg/environment.py:1121-1127,
 // _get_next_car_position_and_route :881-968, _should_car_move :678-691, traffic lights :664-676,
-// _spawn_new_car :970-1002).  Survivors go to the other bank in order, respawned cars are appended
-// after them in creation order; occupancy counters follow every move so later cars see earlier ones.
+// _spawn_new_car :970-1002).  Survivors keep their slots, respawned cars are appended behind the
+// tail in creation order (slot order = list order); occupancy counters follow every move so later
+// cars see earlier ones.
 template <typename T>
 __device__ __forceinline__ T sel4(int k, T a0, T a1, T a2, T a3) {
   return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
@@ -1164,188 +1165,202 @@ __device__ __forceinline__ T sel4(int k, T a0, T a1, T a2, T a3) {
 // the four neighbours, the first admissible one, light and occupancy there) is computed branch-free
 // first; the random draws then go through five draw slots shared by all outcomes (a lane's draws
 // keep numpy's order: delay?, delay length | speed, route | spawner | light, go | profile, route).
-// Exact number of cars on lane slot s while car r leaves it: the cars already moved this tick
-// (survivors [0, w) and respawns [n0 - nnew, n0) of the next bank) and those still to move (r, n0).
-__device__ __noinline__ int recount_slot(const DevCfg& c, const Plan& pl, const CarStore& cs, int cur, int nxt,
-                                         int r, int n0, int w, int nnew, int s) {
-  const int cap = c.car_cap;
+// Exact number of cars on lane slot s while the car in slot r leaves it: slots [0, w) hold the cars
+// already moved this tick (w = r, or the packed count when the tick packs), (r, tail0) those still
+// to move, [tail0, t_out) this tick's respawns.  Rare: only once a 4-bit occupancy counter saturated.
+__device__ __noinline__ int recount_slot(const DevCfg& c, const Plan& pl, const CarSlots& cs, int r, int w, int t_out,
+                                         int s) {
   int n = 0;
-  // three index ranges of two banks (they overlap in index space, not in cars)
-  for (int part = 0; part < 3; part++) {
-    const int bank = part < 2 ? nxt : cur;
-    const int k0 = part == 0 ? 0 : (part == 1 ? n0 - nnew : r + 1);
-    const int k1 = part == 0 ? w : n0;
-    for (int k = k0; k < k1; k++) {
-      const uint32_t w0 = cs.w0[cs.at(bank, cap, k)];
-      n += lane_slot(c, pl, (int)(w0 & 255u), (int)((w0 >> 8) & 255u)) == s ? 1 : 0;
-    }
+  for (int k = 0; k < t_out; k++) {
+    if (k >= w && k <= r) continue;
+    const uint32_t w0 = cs.w0[cs.at(k)];
+    if (w0 & kCarEmpty) continue;
+    n += lane_slot(c, pl, (int)(w0 & 255u), (int)((w0 >> 8) & 255u)) == s ? 1 : 0;
   }
   return n;
 }
 
+// Empty slots an env may start a tick with before its wave packs the slots.  A wave iterates up to
+// its longest list's tail, so empty slots cost every lane an iteration; a packing tick costs the
+// wave an id read and write per car and scattered survivor writes for envs with empty slots.  A/B
+// on configs[2] (k_env<true> + k_traffic per launch): slack 16 1464 us, 8 1456, 4 1402, 0 1450.
+#ifndef PGTG_SLACK
+#define PGTG_SLACK 4
+#endif
+constexpr int kCompactSlack = PGTG_SLACK;
+
+// The car pass.  Slots are visited in order and all lanes of a wave are at the same slot, so the
+// loads and the in-place stores of the survivors are coalesced rows (ids are neither read nor
+// rewritten).  A despawned car leaves an empty slot; its replacement is appended behind the tail.
+// A tick in which some env of the wave starts with more than kCompactSlack empty slots packs instead:
+// survivors are written to the next packed slot w <= r (with their ids), the respawns moved down
+// behind them at the end.
 __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uint64_t i, const EnvView& v,
                                          const Plan& pl, uint8_t* occ, bool& sat, const uint16_t* sp, TrafState& ts,
                                          Pcg& cr, int color, BrakeQuery& bq, uint8_t* hist) {
-  CarStore cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
-  const int cap = c.car_cap, cur = (int)ts.bank, nxt = cur ^ 1;
-  const int n0 = (int)ts.n_cars;
+  const CarSlots cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
   const int tw = c.tw, th = c.th;
   const uint32_t nsp = ts.n_spawners;
-  int w = 0, nnew = 0;
-  // software pipeline: the next car's words are requested before the current car is processed, so
-  // their HBM latency overlaps this car's work (the loop-carried copy waits only at the iteration end)
-  // slot indices advance by the env stride (no 64-bit multiply per car): the car read, the next
-  // survivor slot and the next respawn slot (respawns are written from the end backwards)
+  const int tail0 = (int)ts.tail;
+  // (wave-uniform: packing is right for any list, and a uniform flag keeps the loop free of
+  // exec-mask juggling around the packing writes)
+  const bool pack = __any(tail0 > (int)ts.n_cars + kCompactSlack);
+  int t_out = tail0, w = 0;
   const uint64_t nst = S.n;
-  uint64_t ar = cs.at(cur, cap, 0), aw_i = cs.at(nxt, cap, 0), an_i = cs.at(nxt, cap, n0 - 1);
-  uint32_t na, npat, nid;
-  na = cs.w0[ar];
-  npat = cs.w1[ar];
-  nid = cs.id[ar];
-  for (int r = 0; r < n0; r++) {
+  // software pipeline: the next slot's words are requested before the current car is processed, so
+  // their HBM latency overlaps this car's work (slot indices advance by the env stride)
+  uint64_t ar = cs.at(0), an = cs.at(tail0), ap = cs.at(0);
+  uint32_t na = cs.w0[ar], npat = cs.w1[ar], nid = 0u;
+  if (pack) nid = cs.id[ar];
+  for (int r = 0; r < tail0; r++) {
+    const uint64_t aw = ar;
     const uint32_t a = na, id = nid;
     uint32_t pat = npat;
-    if (r + 1 < n0) ar += nst;
+    if (r + 1 < tail0) ar += nst;
     na = cs.w0[ar];
     npat = cs.w1[ar];
-    nid = cs.id[ar];
-    const int x = (int)(a & 255u), y = (int)((a >> 8) & 255u), prof = (int)((a >> 21) & 7u);
-    int route = (int)((a >> 16) & 31u), delay = (int)((a >> 24) & 3u);
-    // ---- map lookups (no draws)
-    const int tx = x / kTile, ty = y / kTile, lx = x - tx * kTile, ly = y - ty * kTile;
-    const int t0 = ty * tw + tx, sq = lx * 9 + ly;
-    const int s_old = t0 * 32 + sT.li[plan_exits(pl[t0])][sq];
-    // neighbours up, down, left, right (_get_next_car_position_and_route's order)
-    const bool ok0 = !(ly == 0 && ty == 0), ok1 = !(ly == 8 && ty == th - 1);
-    const bool ok2 = !(lx == 0 && tx == 0), ok3 = !(lx == 8 && tx == tw - 1);
-    const int nt0 = ly == 0 ? t0 - tw : t0, nt1 = ly == 8 ? t0 + tw : t0;
-    const int nt2 = lx == 0 ? t0 - 1 : t0, nt3 = lx == 8 ? t0 + 1 : t0;
-    const int nq0 = ly == 0 ? sq + 8 : sq - 1, nq1 = ly == 8 ? sq - 8 : sq + 1;
-    const int nq2 = lx == 0 ? sq + 72 : sq - 9, nq3 = lx == 8 ? sq - 72 : sq + 9;
-    const uint32_t e0 = ok0 ? plan_exits(pl[nt0]) : 0u, e1 = ok1 ? plan_exits(pl[nt1]) : 0u;
-    const uint32_t e2 = ok2 ? plan_exits(pl[nt2]) : 0u, e3 = ok3 ? plan_exits(pl[nt3]) : 0u;
-    const uint32_t l0 = e0 ? sT.lanes[e0][nq0] : 0u, l1 = e1 ? sT.lanes[e1][nq1] : 0u;
-    const uint32_t l2 = e2 ? sT.lanes[e2][nq2] : 0u, l3 = e3 ? sT.lanes[e3][nq3] : 0u;
-    const uint32_t rtl = *reinterpret_cast<const uint32_t*>(sT.route_type_lane[route]);
-    int dec = -1;
-    bool dec_all = false;
+    if (pack) nid = cs.id[ar];
+    if (!(a & kCarEmpty)) {
+      const int x = (int)(a & 255u), y = (int)((a >> 8) & 255u), prof = (int)((a >> 21) & 7u);
+      int route = (int)((a >> 16) & 31u), delay = (int)((a >> 24) & 3u);
+      // ---- map lookups (no draws)
+      const int tx = x / kTile, ty = y / kTile, lx = x - tx * kTile, ly = y - ty * kTile;
+      const int t0 = ty * tw + tx, sq = lx * 9 + ly;
+      const int s_old = t0 * 32 + sT.li[plan_exits(pl[t0])][sq];
+      // neighbours up, down, left, right (_get_next_car_position_and_route's order)
+      const bool ok0 = !(ly == 0 && ty == 0), ok1 = !(ly == 8 && ty == th - 1);
+      const bool ok2 = !(lx == 0 && tx == 0), ok3 = !(lx == 8 && tx == tw - 1);
+      const int nt0 = ly == 0 ? t0 - tw : t0, nt1 = ly == 8 ? t0 + tw : t0;
+      const int nt2 = lx == 0 ? t0 - 1 : t0, nt3 = lx == 8 ? t0 + 1 : t0;
+      const int nq0 = ly == 0 ? sq + 8 : sq - 1, nq1 = ly == 8 ? sq - 8 : sq + 1;
+      const int nq2 = lx == 0 ? sq + 72 : sq - 9, nq3 = lx == 8 ? sq - 72 : sq + 9;
+      const uint32_t e0 = ok0 ? plan_exits(pl[nt0]) : 0u, e1 = ok1 ? plan_exits(pl[nt1]) : 0u;
+      const uint32_t e2 = ok2 ? plan_exits(pl[nt2]) : 0u, e3 = ok3 ? plan_exits(pl[nt3]) : 0u;
+      const uint32_t l0 = e0 ? sT.lanes[e0][nq0] : 0u, l1 = e1 ? sT.lanes[e1][nq1] : 0u;
+      const uint32_t l2 = e2 ? sT.lanes[e2][nq2] : 0u, l3 = e3 ? sT.lanes[e3][nq3] : 0u;
+      const uint32_t rtl = *reinterpret_cast<const uint32_t*>(sT.route_type_lane[route]);
+      int dec = -1;
+      bool dec_all = false;
 #pragma unroll
-    for (int t = 3; t >= 0; t--) {  // the first direction with a lane "all <t>" or the route's lane
-      const uint32_t ln = sel4(t, l0, l1, l2, l3);
-      const bool all = (ln >> (28 + t)) & 1u;
-      const uint32_t lane = (rtl >> (8 * t)) & 255u;
-      const bool rt = lane != 255u && ((ln >> lane) & 1u);
-      if (all || rt) {
-        dec = t;
-        dec_all = all;
+      for (int t = 3; t >= 0; t--) {  // the first direction with a lane "all <t>" or the route's lane
+        const uint32_t ln = sel4(t, l0, l1, l2, l3);
+        const bool all = (ln >> (28 + t)) & 1u;
+        const uint32_t lane = (rtl >> (8 * t)) & 255u;
+        const bool rt = lane != 255u && ((ln >> lane) & 1u);
+        if (all || rt) {
+          dec = t;
+          dec_all = all;
+        }
       }
-    }
-    const int dk = dec < 0 ? 0 : dec;
-    const int tg_t = sel4(dk, nt0, nt1, nt2, nt3), tg_q = sel4(dk, nq0, nq1, nq2, nq3);
-    const uint32_t tg_ln = sel4(dk, l0, l1, l2, l3);
-    const uint32_t p_tg = pl[dec < 0 ? t0 : tg_t];
-    const uint32_t ex_tg = plan_exits(p_tg);
-    const bool tl = plan_otype(p_tg) == 4u && !bit81(sT.wall[ex_tg], tg_q) && bit81(sT.obst[plan_omask(p_tg)], tg_q);
-    const int s_tg = tg_t * 32 + sT.li[ex_tg][tg_q];
-    const int occ_tg = dec < 0 ? 0 : occ_get(occ, s_tg);
-    // ---- draws (_should_car_move, route choice / light / following, _spawn_new_car)
-    const bool act = delay == 0;
-    bool delayed = false, move = false;
-    if (act) {
-      delayed = pcg_draw(cr, false, 0u) < sT.beh_t[BEH_DELAY][prof];
-      const uint64_t r2 = pcg_draw(cr, delayed, 3u);
-      if (delayed) delay = 1 + (int)r2;  // integers(1, 4)
-      else move = r2 < sT.beh_t[BEH_SPEED][prof];
-    } else {
-      delay -= 1;
-    }
-    const int kind = !move ? 0 : (dec < 0 ? 3 : (dec_all ? 1 : 2));  // stay, all-lane, route lane, respawn
-    const uint32_t nr_all = __popc(tg_ln & 0x0fffffffu);
-    if (kind == 1 && nr_all == 0) return PGTG_E_MAP;  // numpy choice([]) raises
-    const bool lit = kind == 2 && tl && color != 0;
-    const bool s3_int = kind != 2;
-    const uint32_t s3_n = kind == 1 ? nr_all : nsp;
-    uint64_t r3 = 0;
-    if ((kind == 1 || kind == 3 || lit) && !(s3_int && s3_n <= 1u)) r3 = pcg_draw(cr, s3_int, s3_n);
-    const bool stop = lit && (color == 1 ? r3 < sT.beh_t[BEH_YELLOW][prof] : !(r3 < sT.beh_t[BEH_RED][prof]));
-    const bool go_try = kind == 2 && !stop && occ_tg > 0 && (sT.beh_mf[prof] == 0 || (int)pat > sT.beh_pt[prof]);
-    uint64_t r4 = 0;
-    if (go_try || kind == 3) r4 = pcg_draw(cr, false, 0u);
-    if (kind == 3) {
-      // _spawn_new_car: choice(car_spawners) -> sorted routes -> profile -> route
-      if (sat && occ_get(occ, s_old) >= kOccMax)
-        occ_put(occ, s_old, min(recount_slot(c, pl, cs, cur, nxt, r, n0, w, nnew, s_old), kOccMax));
-      else
-        occ_put(occ, s_old, occ_get(occ, s_old) - 1);
-      int sx = 0, sy = 0;
-      if (nsp > 0) {
-        const uint32_t code = r3 < (uint64_t)kSpCache ? sp[r3] : S.spawners[r3 * S.n + i];
-        sx = (int)(code & 255u);
-        sy = (int)(code >> 8);
-      }
-      const uint32_t rl = square_lanes(c, pl, sx, sy) & 0x0fffffffu;
-      const uint32_t nr = __popc(rl);
-      int nprof = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) nprof += (r4 < c.profile_t[j]) ? 0 : 1;
-      if (nr == 0) return PGTG_E_MAP;
-      const uint32_t r5 = nr > 1u ? (uint32_t)pcg_draw(cr, true, nr) : 0u;
-      const int nroute = sT.lane_route[kth_bit(rl, (int)r5)];
-      const uint64_t an = an_i;
-      an_i -= nst;
-      cs.w0[an] = (uint32_t)sx | (uint32_t)sy << 8 | (uint32_t)nroute << 16 | (uint32_t)nprof << 21;
-      cs.w1[an] = 0u;
-      cs.id[an] = ts.next_id++;
-      nnew++;
-      const int s_new = lane_slot(c, pl, sx, sy);
-      if (s_new < 0) return PGTG_E_UNSUPPORTED;
-      occ_inc(occ, s_new, sat);
-      if (bq.tile >= 0 && (s_new >> 5) == bq.tile) {
-        bq.n_in++;
-        hist[nroute]++;
-      }
-    } else {
-      const bool go = go_try && r4 < sT.beh_t[BEH_GO][prof];
-      const bool moved = kind == 1 || (kind == 2 && !stop && (occ_tg == 0 || go));
-      if (kind == 1) route = sT.lane_route[kth_bit(tg_ln & 0x0fffffffu, (int)r3)];
-      int nx = x, ny = y, s_cur = s_old;
-      if (moved) {
-        nx = x + (dk == 2 ? -1 : (dk == 3 ? 1 : 0));
-        ny = y + (dk == 0 ? -1 : (dk == 1 ? 1 : 0));
-        if (sat && occ_get(occ, s_old) >= kOccMax)
-          occ_put(occ, s_old, min(recount_slot(c, pl, cs, cur, nxt, r, n0, w, nnew, s_old), kOccMax));
-        else
-          occ_put(occ, s_old, occ_get(occ, s_old) - 1);
-        s_cur = s_tg;
-        occ_inc(occ, s_cur, sat);
-        pat = 0;
+      const int dk = dec < 0 ? 0 : dec;
+      const int tg_t = sel4(dk, nt0, nt1, nt2, nt3), tg_q = sel4(dk, nq0, nq1, nq2, nq3);
+      const uint32_t tg_ln = sel4(dk, l0, l1, l2, l3);
+      const uint32_t p_tg = pl[dec < 0 ? t0 : tg_t];
+      const uint32_t ex_tg = plan_exits(p_tg);
+      const bool tl = plan_otype(p_tg) == 4u && !bit81(sT.wall[ex_tg], tg_q) && bit81(sT.obst[plan_omask(p_tg)], tg_q);
+      const int s_tg = tg_t * 32 + sT.li[ex_tg][tg_q];
+      const int occ_tg = dec < 0 ? 0 : occ_get(occ, s_tg);
+      // ---- draws (_should_car_move, route choice / light / following, _spawn_new_car)
+      const bool act = delay == 0;
+      bool delayed = false, move = false;
+      if (act) {
+        delayed = pcg_draw(cr, false, 0u) < sT.beh_t[BEH_DELAY][prof];
+        const uint64_t r2 = pcg_draw(cr, delayed, 3u);
+        if (delayed) delay = 1 + (int)r2;  // integers(1, 4)
+        else move = r2 < sT.beh_t[BEH_SPEED][prof];
       } else {
-        pat += 1;
+        delay -= 1;
       }
-      if (bq.tile >= 0 && (s_cur >> 5) == bq.tile) {
-        bq.n_in++;
-        hist[route]++;
+      const int kind = !move ? 0 : (dec < 0 ? 3 : (dec_all ? 1 : 2));  // stay, all-lane, route lane, respawn
+      const uint32_t nr_all = __popc(tg_ln & 0x0fffffffu);
+      if (kind == 1 && nr_all == 0) return PGTG_E_MAP;  // numpy choice([]) raises
+      const bool lit = kind == 2 && tl && color != 0;
+      const bool s3_int = kind != 2;
+      const uint32_t s3_n = kind == 1 ? nr_all : nsp;
+      uint64_t r3 = 0;
+      if ((kind == 1 || kind == 3 || lit) && !(s3_int && s3_n <= 1u)) r3 = pcg_draw(cr, s3_int, s3_n);
+      const bool stop = lit && (color == 1 ? r3 < sT.beh_t[BEH_YELLOW][prof] : !(r3 < sT.beh_t[BEH_RED][prof]));
+      const bool go_try = kind == 2 && !stop && occ_tg > 0 && (sT.beh_mf[prof] == 0 || (int)pat > sT.beh_pt[prof]);
+      uint64_t r4 = 0;
+      if (go_try || kind == 3) r4 = pcg_draw(cr, false, 0u);
+      const bool leaves = kind == 3 || kind == 1 || (kind == 2 && !stop && (occ_tg == 0 || (go_try && r4 < sT.beh_t[BEH_GO][prof])));
+      if (leaves) {  // the car's square loses it
+        if (sat && occ_get(occ, s_old) >= kOccMax) {
+          // exact recount from HBM (this car's slot still holds its old square)
+          occ_put(occ, s_old, min(recount_slot(c, pl, cs, r, pack ? w : r, t_out, s_old), kOccMax));
+        } else {
+          occ_put(occ, s_old, occ_get(occ, s_old) - 1);
+        }
       }
-      const uint64_t aw = aw_i;
-      aw_i += nst;
-      cs.w0[aw] = (uint32_t)nx | (uint32_t)ny << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21 | (uint32_t)delay << 24;
-      cs.w1[aw] = pat;
-      cs.id[aw] = id;
-      w++;
+      if (kind == 3) {
+        // _spawn_new_car: choice(car_spawners) -> sorted routes -> profile -> route
+        int sx = 0, sy = 0;
+        if (nsp > 0) {
+          const uint32_t code = r3 < (uint64_t)kSpCache ? sp[r3] : S.spawners[r3 * S.n + i];
+          sx = (int)(code & 255u);
+          sy = (int)(code >> 8);
+        }
+        const uint32_t rl = square_lanes(c, pl, sx, sy) & 0x0fffffffu;
+        const uint32_t nr = __popc(rl);
+        int nprof = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) nprof += (r4 < c.profile_t[q]) ? 0 : 1;
+        if (nr == 0) return PGTG_E_MAP;
+        const uint32_t r5 = nr > 1u ? (uint32_t)pcg_draw(cr, true, nr) : 0u;
+        const int nroute = sT.lane_route[kth_bit(rl, (int)r5)];
+        if (!pack) cs.w0[aw] = kCarEmpty;
+        cs.w0[an] = (uint32_t)sx | (uint32_t)sy << 8 | (uint32_t)nroute << 16 | (uint32_t)nprof << 21;
+        cs.w1[an] = 0u;
+        cs.id[an] = ts.next_id++;
+        an += nst;
+        t_out++;
+        const int s_new = lane_slot(c, pl, sx, sy);
+        if (s_new < 0) return PGTG_E_UNSUPPORTED;
+        occ_inc(occ, s_new, sat);
+        if (bq.tile >= 0 && (s_new >> 5) == bq.tile) {
+          bq.n_in++;
+          hist[nroute]++;
+        }
+      } else {
+        if (kind == 1) route = sT.lane_route[kth_bit(tg_ln & 0x0fffffffu, (int)r3)];
+        int nx = x, ny = y, s_cur = s_old;
+        if (leaves) {
+          nx = x + (dk == 2 ? -1 : (dk == 3 ? 1 : 0));
+          ny = y + (dk == 0 ? -1 : (dk == 1 ? 1 : 0));
+          s_cur = s_tg;
+          occ_inc(occ, s_cur, sat);
+          pat = 0;
+        } else {
+          pat += 1;
+        }
+        if (bq.tile >= 0 && (s_cur >> 5) == bq.tile) {
+          bq.n_in++;
+          hist[route]++;
+        }
+        const uint64_t ao = pack ? ap : aw;
+        cs.w0[ao] = (uint32_t)nx | (uint32_t)ny << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21 | (uint32_t)delay << 24;
+        cs.w1[ao] = pat;
+        if (pack) {
+          cs.id[ao] = id;
+          ap += nst;
+          w++;
+        }
+      }
     }
   }
-  // respawned cars were written from the end backwards: restore creation order
-  for (int j = 0; j < nnew / 2; j++) {
-    const uint64_t p1 = cs.at(nxt, cap, w + j), p2 = cs.at(nxt, cap, n0 - 1 - j);
-    uint32_t t0 = cs.w0[p1], t1 = cs.w1[p1], t2 = cs.id[p1];
-    cs.w0[p1] = cs.w0[p2];
-    cs.w1[p1] = cs.w1[p2];
-    cs.id[p1] = cs.id[p2];
-    cs.w0[p2] = t0;
-    cs.w1[p2] = t1;
-    cs.id[p2] = t2;
+  if (pack) {  // this tick's respawns, [tail0, t_out), moved down behind the packed survivors
+    uint64_t as = cs.at(tail0);
+    for (int k = tail0; k < t_out; k++) {
+      const uint32_t x0 = cs.w0[as], x1 = cs.w1[as], x2 = cs.id[as];
+      cs.w0[ap] = x0;
+      cs.w1[ap] = x1;
+      cs.id[ap] = x2;
+      as += nst;
+      ap += nst;
+    }
+    t_out = w + (t_out - tail0);
   }
-  ts.bank = (uint32_t)nxt;
+  ts.tail = (uint32_t)t_out;
   return 0;
 }
 
@@ -1782,24 +1797,25 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       ts.n_cars = tr4.x & 0xffffu;
       ts.n_spawners = tr4.x >> 16;
       ts.next_id = tr4.y;
-      ts.bank = tr4.z;
+      ts.tail = tr4.z;
     }
     stage_plan(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, L.plan_stride_dw);
   }
   for (int k = tid; k < L.lm_words; k += kBlock) lm[k] = 0u;
   lds_barrier();  // sT ready
   if (live && (TR && c.need_car)) {
-    // occupancy counters from the current car positions (one coalesced slot row per car index)
+    // occupancy counters from the current car positions (one coalesced slot row per slot index, 16
+    // loads in flight per lane)
     for (int w = 0; w < c.nt * 4; w++) traf_w[w] = 0u;  // 16 B of 4-bit counters per tile
-    CarStore cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
-    const int nc = (int)ts.n_cars;
-    for (int k0 = 0; k0 < nc; k0 += 16) {  // 16 independent loads in flight per lane
+    const CarSlots cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
+    const int tail = (int)ts.tail;
+    for (int k0 = 0; k0 < tail; k0 += 16) {
       uint32_t a16[16];
 #pragma unroll
-      for (int g = 0; g < 16; g++) a16[g] = cs.w0[cs.at((int)ts.bank, c.car_cap, k0 + g < nc ? k0 + g : 0)];
+      for (int g = 0; g < 16; g++) a16[g] = cs.w0[cs.at(k0 + g < tail ? k0 + g : 0)];
 #pragma unroll
       for (int g = 0; g < 16; g++) {
-        if (k0 + g < nc) {
+        if (k0 + g < tail && !(a16[g] & kCarEmpty)) {
           int sl = lane_slot(c, pl, (int)(a16[g] & 255u), (int)((a16[g] >> 8) & 255u));
           if (sl < 0) err = PGTG_E_UNSUPPORTED;
           else occ_inc(occ, sl, occ_sat);
@@ -1949,7 +1965,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (live) {
     if (mode != MODE_OBSERVE) {
       rec_store(S.rec, i, v);
-      if ((TR && c.need_car)) S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.bank, 0u);
+      if ((TR && c.need_car)) S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.tail, 0u);
     }
     if (mode != MODE_OBSERVE || err) S.err[i] = (uint8_t)(-err);
     if (S.qstate && reset_now) S.qstate[i] = 0;  // maps generated here: the queued ones are stale
@@ -2341,7 +2357,7 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
     const int err = traffic_reset(c, S, i, pl, cr, rs, ts, at, CR, sub, g);
     if (sub == 0) {
       stream_store_state(S.car, i, cr);
-      S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.bank, 0u);
+      S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.tail, 0u);
       if (err) S.err[i] = (uint8_t)(-err);
       if (c.obs_fast && c.traffic_ch >= 0 && out.obs) {
         // the tile window's traffic channel: k_env wrote it with no cars; set the car squares
@@ -2698,6 +2714,13 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
     if (cap < in.min_car_capacity) cap = in.min_car_capacity;
     if (cap < 1) cap = 1;
     c.car_cap = cap;
+    // one bank: a tick starts with at most 2 x cap + kCompactSlack slots in use (a tick that does not
+    // pack starts with <= cap + kCompactSlack and appends <= cap respawns) and appends <= cap more
+    c.car_slots = 3 * cap + kCompactSlack;  // configs[2]: 1 204 slots x 12 B x 65 536 envs = 947 MB
+    if (in.tune_car_slots > 0) {
+      if (in.tune_car_slots < c.car_slots) return fail(h, PGTG_E_INVALID, "tune_car_slots < 3 x car capacity + 4");
+      c.car_slots = in.tune_car_slots;
+    }
     c.max_spawners = c.nt * 5;
     // k_env: occupancy counters (nt * 32 lane slots, 4 bit) then the spawner cache
     c.sp_cache_off = c.nt * 16;
@@ -2904,9 +2927,9 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     }
   if (c.visited_penalty != 0.0) ALLOC(S.visited, n * (uint64_t)c.vis_words);
   if (c.need_car) {
-    ALLOC(S.car_w0, 2 * (uint64_t)c.car_cap * n);
-    ALLOC(S.car_w1, 2 * (uint64_t)c.car_cap * n);
-    ALLOC(S.car_id, 2 * (uint64_t)c.car_cap * n);
+    ALLOC(S.car_w0, (uint64_t)c.car_slots * n);
+    ALLOC(S.car_w1, (uint64_t)c.car_slots * n);
+    ALLOC(S.car_id, (uint64_t)c.car_slots * n);
     ALLOC(S.traf, n);
     ALLOC(S.spawners, (uint64_t)c.max_spawners * n);
     ALLOC(S.tr_list, n);
@@ -3144,10 +3167,57 @@ int pgtg_get_env_state(pgtg_handle* h, uint64_t env, PgtgEnvState* st) {
     st->n_cars = (int)(t.x & 0xffffu);
     st->n_spawners = (int)(t.x >> 16);
     st->next_car_id = (int)t.y;
+    st->car_tail = (int)t.z;
   }
   return PGTG_OK;
 }
 
+
+// One env's cars in list order (empty slots skipped): a strided copy of its slots.
+static int host_read_cars(pgtg_handle* h, uint64_t env, const uint4& t, std::vector<PgtgCar>& cars) {
+  cars.clear();
+  const int tail = (int)t.z;
+  if (tail == 0) return 0;
+  const uint64_t N = h->n;
+  std::vector<uint32_t> w0(tail), w1(tail), id(tail);
+  HIPCHK(h, hipMemcpy2D(w0.data(), 4, h->S.car_w0 + env, N * 4, 4, tail, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy2D(w1.data(), 4, h->S.car_w1 + env, N * 4, 4, tail, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy2D(id.data(), 4, h->S.car_id + env, N * 4, 4, tail, hipMemcpyDeviceToHost));
+  for (int k = 0; k < tail; k++) {
+    if (w0[k] & kCarEmpty) continue;
+    cars.push_back(PgtgCar{(int32_t)id[k], (int32_t)(w0[k] & 255u), (int32_t)((w0[k] >> 8) & 255u),
+                           (int32_t)((w0[k] >> 16) & 31u), (int32_t)((w0[k] >> 21) & 7u), (int32_t)w1[k],
+                           (int32_t)((w0[k] >> 24) & 3u)});
+  }
+  if ((int)cars.size() != (int)(t.x & 0xffffu)) return fail(h, PGTG_E_DEVICE, "car slots disagree with the car count");
+  return 0;
+}
+
+// One env's car list written packed into slots [0, n); the traffic record gets n cars, tail n and
+// next id `next_id`.
+static int host_write_cars(pgtg_handle* h, uint64_t env, uint4 t, const std::vector<PgtgCar>& cars, uint32_t next_id) {
+  const int n = (int)cars.size();
+  if (n > h->hcfg.car_cap) return fail(h, PGTG_E_UNSUPPORTED, "more cars than the handle's car capacity");
+  const uint64_t N = h->n;
+  std::vector<uint32_t> w0(n), w1(n), id(n);
+  for (int k = 0; k < n; k++) {
+    const PgtgCar& q = cars[k];
+    w0[k] = (uint32_t)q.x | (uint32_t)q.y << 8 | (uint32_t)q.route << 16 | (uint32_t)q.profile << 21 |
+            (uint32_t)q.delay << 24;
+    w1[k] = (uint32_t)q.patience;
+    id[k] = (uint32_t)q.id;
+  }
+  if (n > 0) {
+    HIPCHK(h, hipMemcpy2D(h->S.car_w0 + env, N * 4, w0.data(), 4, 4, n, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy2D(h->S.car_w1 + env, N * 4, w1.data(), 4, 4, n, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy2D(h->S.car_id + env, N * 4, id.data(), 4, 4, n, hipMemcpyHostToDevice));
+  }
+  t.x = (t.x & 0xffff0000u) | (uint32_t)n;
+  t.y = next_id;
+  t.z = (uint32_t)n;
+  HIPCHK(h, hipMemcpy(h->S.traf + env, &t, sizeof t, hipMemcpyHostToDevice));
+  return 0;
+}
 
 int pgtg_get_cars(pgtg_handle* h, uint64_t env, PgtgCar* cars, int32_t cap, int32_t* n) {
   if (!h || env >= h->n || !n) return PGTG_E_INVALID;
@@ -3157,21 +3227,11 @@ int pgtg_get_cars(pgtg_handle* h, uint64_t env, PgtgCar* cars, int32_t cap, int3
   HIPCHK(h, hipStreamSynchronize(h->stream));
   uint4 t;
   if (int rc = read_traf(h, env, &t)) return rc;
-  int nc = (int)(t.x & 0xffffu), bank = (int)t.z;
-  *n = nc;
-  const uint64_t N = h->n, C = (uint64_t)h->hcfg.car_cap;
-  const int m = nc < cap ? nc : cap;
-  if (cars && m > 0) {
-    // one strided copy per array: slot k of env `env` lives at ((bank*C + k)*N + env)
-    std::vector<uint32_t> w0(m), w1(m), id(m);
-    const uint64_t base = (uint64_t)bank * C * N + env;
-    HIPCHK(h, hipMemcpy2D(w0.data(), 4, h->S.car_w0 + base, N * 4, 4, m, hipMemcpyDeviceToHost));
-    HIPCHK(h, hipMemcpy2D(w1.data(), 4, h->S.car_w1 + base, N * 4, 4, m, hipMemcpyDeviceToHost));
-    HIPCHK(h, hipMemcpy2D(id.data(), 4, h->S.car_id + base, N * 4, 4, m, hipMemcpyDeviceToHost));
-    for (int k = 0; k < m; k++)
-      cars[k] = PgtgCar{(int32_t)id[k], (int32_t)(w0[k] & 255u), (int32_t)((w0[k] >> 8) & 255u),
-                        (int32_t)((w0[k] >> 16) & 31u), (int32_t)((w0[k] >> 21) & 7u), (int32_t)w1[k],
-                        (int32_t)((w0[k] >> 24) & 3u)};
+  *n = (int)(t.x & 0xffffu);
+  if (cars && cap > 0 && *n > 0) {
+    std::vector<PgtgCar> v;
+    if (int rc = host_read_cars(h, env, t, v)) return rc;
+    for (int k = 0; k < (int)v.size() && k < cap; k++) cars[k] = v[k];
   }
   return PGTG_OK;
 }
@@ -3276,23 +3336,17 @@ int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t rou
   HIPCHK(h, hipStreamSynchronize(h->stream));
   uint4 t;
   if (int rc = read_traf(h, env, &t)) return rc;
-  int nc = (int)(t.x & 0xffffu), bank = (int)t.z;
-  if (nc >= h->hcfg.car_cap) return fail(h, PGTG_E_UNSUPPORTED, "car capacity exhausted");
-  const uint64_t a = ((uint64_t)bank * h->hcfg.car_cap + nc) * h->n + env;
-  uint32_t w0 = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)profile << 21, w1 = 0;
+  std::vector<PgtgCar> v;
+  if (int rc = host_read_cars(h, env, t, v)) return rc;
+  if ((int)v.size() >= h->hcfg.car_cap) return fail(h, PGTG_E_UNSUPPORTED, "car capacity exhausted");
   const uint32_t id = car_id < 0 ? t.y : (uint32_t)car_id;
-  HIPCHK(h, hipMemcpy(h->S.car_w0 + a, &w0, 4, hipMemcpyHostToDevice));
-  HIPCHK(h, hipMemcpy(h->S.car_w1 + a, &w1, 4, hipMemcpyHostToDevice));
-  HIPCHK(h, hipMemcpy(h->S.car_id + a, &id, 4, hipMemcpyHostToDevice));
-  t.x = (t.x & 0xffff0000u) | (uint32_t)(nc + 1);
-  if (car_id < 0) t.y += 1;
-  HIPCHK(h, hipMemcpy(h->S.traf + env, &t, sizeof t, hipMemcpyHostToDevice));
-  return PGTG_OK;
+  v.push_back(PgtgCar{(int32_t)id, x, y, route, profile, 0, 0});
+  return host_write_cars(h, env, t, v, car_id < 0 ? t.y + 1u : t.y);
 }
 
 // ---- whole-batch state dump / load (bit-exact replay) ----------------------------------------
 // Every device array that carries an env's state from one launch to the next: agent records, seeds,
-// tile plans, error codes, counters, the four RNG streams, the visited bitsets, both car banks, the
+// tile plans, error codes, counters, the four RNG streams, the visited bitsets, the car slots, the
 // traffic records, the spawner lists and the map queue.  The k_traffic work list is per-launch
 // scratch (its counters are zeroed on load).  Blob: PgtgStateHeader, n_sections x {id, pad, bytes},
 // then each section's bytes at a 16-byte aligned offset.
@@ -3307,13 +3361,13 @@ struct PgtgStateHeader {
   uint32_t version;
   uint64_t n;
   uint32_t n_sections, nt, car_cap, plan_stride;
-  uint32_t max_spawners, vis_words, qrec_dw, reserved;
+  uint32_t max_spawners, vis_words, qrec_dw, car_slots;
 };
 struct PgtgSectionEntry {
   uint32_t id, pad;
   uint64_t bytes;
 };
-constexpr uint32_t kStateVersion = 1;
+constexpr uint32_t kStateVersion = 2;
 }  // namespace
 
 static std::vector<StateSection> state_sections(pgtg_handle* h) {
@@ -3338,9 +3392,9 @@ static std::vector<StateSection> state_sections(pgtg_handle* h) {
     add(14 + 5 * k, st[k]->buf, n * 8);
   }
   add(30, S.visited, n * (uint64_t)c.vis_words * 4);
-  add(31, S.car_w0, 2 * (uint64_t)c.car_cap * n * 4);
-  add(32, S.car_w1, 2 * (uint64_t)c.car_cap * n * 4);
-  add(33, S.car_id, 2 * (uint64_t)c.car_cap * n * 4);
+  add(31, S.car_w0, (uint64_t)c.car_slots * n * 4);
+  add(32, S.car_w1, (uint64_t)c.car_slots * n * 4);
+  add(33, S.car_id, (uint64_t)c.car_slots * n * 4);
   add(34, S.traf, n * sizeof(uint4));
   add(35, S.spawners, (uint64_t)c.max_spawners * n * 2);
   add(40, S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw * 4);
@@ -3378,6 +3432,7 @@ int pgtg_dump_state(pgtg_handle* h, void* buf, uint64_t bytes) {
   hd.max_spawners = (uint32_t)h->hcfg.max_spawners;
   hd.vis_words = (uint32_t)h->hcfg.vis_words;
   hd.qrec_dw = (uint32_t)h->hcfg.qrec_dw;
+  hd.car_slots = (uint32_t)h->hcfg.car_slots;
   memcpy(p, &hd, sizeof hd);
   uint64_t off = sizeof hd;
   for (const auto& s : v) {
@@ -3405,7 +3460,8 @@ int pgtg_load_state(pgtg_handle* h, const void* buf, uint64_t bytes) {
   if (hd.n != h->n || hd.n_sections != v.size() || hd.nt != (uint32_t)h->hcfg.nt ||
       hd.car_cap != (uint32_t)h->hcfg.car_cap || hd.plan_stride != (uint32_t)h->hcfg.plan_stride ||
       hd.max_spawners != (uint32_t)h->hcfg.max_spawners || hd.vis_words != (uint32_t)h->hcfg.vis_words ||
-      hd.qrec_dw != (uint32_t)h->hcfg.qrec_dw || bytes < state_blob_bytes(v))
+      hd.qrec_dw != (uint32_t)h->hcfg.qrec_dw || hd.car_slots != (uint32_t)h->hcfg.car_slots ||
+      bytes < state_blob_bytes(v))
     return fail(h, PGTG_E_INVALID, "pgtg_load_state: the state was dumped from a handle of another shape");
   uint64_t off = sizeof hd;
   for (const auto& s : v) {
@@ -3455,18 +3511,9 @@ int pgtg_set_to_state(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_
   if (c.need_car) {
     uint4 t;
     if (int rc = read_traf(h, env, &t)) return rc;
-    const int bank = (int)t.z, nc = n_cars > 0 ? n_cars : 0;
-    for (int k = 0; k < nc; k++) {
-      const uint64_t a = ((uint64_t)bank * c.car_cap + k) * h->n + env;
-      const uint32_t w0 = (uint32_t)cars[k].x | (uint32_t)cars[k].y << 8 | (uint32_t)cars[k].route << 16 |
-                          (uint32_t)cars[k].profile << 21, w1 = 0, id = (uint32_t)cars[k].id;
-      HIPCHK(h, hipMemcpy(h->S.car_w0 + a, &w0, 4, hipMemcpyHostToDevice));
-      HIPCHK(h, hipMemcpy(h->S.car_w1 + a, &w1, 4, hipMemcpyHostToDevice));
-      HIPCHK(h, hipMemcpy(h->S.car_id + a, &id, 4, hipMemcpyHostToDevice));
-    }
-    t.x = (t.x & 0xffff0000u) | (uint32_t)nc;
-    if (nc > 0) t.y = (uint32_t)cars[nc - 1].id + 1u;
-    HIPCHK(h, hipMemcpy(h->S.traf + env, &t, sizeof t, hipMemcpyHostToDevice));
+    std::vector<PgtgCar> v;
+    for (int k = 0; k < n_cars; k++) v.push_back(PgtgCar{cars[k].id, cars[k].x, cars[k].y, cars[k].route, cars[k].profile, 0, 0});
+    if (int rc = host_write_cars(h, env, t, v, n_cars > 0 ? (uint32_t)cars[n_cars - 1].id + 1u : t.y)) return rc;
   }
   return PGTG_OK;
 }
