@@ -1058,6 +1058,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
       if (t == st_t && ((ex >> st_d) & 1u)) ST[k] = sT.seg[st_d][k];
       if (ot) OB[k] = sT.obst[plan_omask(p)][k] & ~W3[k];
     }
+    STAMP(19);
     for (int ci = 0; ci < c.n_channels; ci++) {
       int code = c.channels[ci];
       uint32_t out3[3];
@@ -1122,6 +1123,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
       }
     }
   }
+  STAMP(20);
   sink.finish();
   oi.nsd = -1;
   if (c.next_subgoal) {
@@ -1136,6 +1138,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
     }
     oi.nsd = nsd;
   }
+  STAMP(21);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2176,6 +2179,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     bool occ_sat = false;
     TrafState ts{0, 0, 0, 0};
     err = env_step<false>(c, S, i, v, pl, actions[i], res, nullptr, occ_sat, nullptr, ts, nullptr);
+    STAMP(22);
     const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
     if (out.reward) out.reward[i] = res.reward;
     if (out.cost) out.cost[i] = res.cost;
@@ -2185,6 +2189,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
     if (lm && my_sel && out.final_obs) mark_lines(lm, out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)slot, (uint32_t)c.obs_bytes);
     ObsInfo oi;  // the post-step image of every env (terminal for the finished ones)
+    STAMP(23);
     build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
 #ifdef PGTG_TUNING
     if (L.diag == 9) build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);  // diagnostic

@@ -24,7 +24,9 @@ SUB = {"cars": (16, 17), "braking": (17, 18), "reset.seed": (8, 9), "reset.gener
        "gen.removal": (14, 15), "gen.tiles": (15, 10), "traf.spawners": (19, 20), "traf.floyd": (20, 21),
        "traf.shuffle": (21, 22), "traf.lookup": (22, 26), "traf.create": (26, 23),
        "final.build": (2, 28), "final.barrier": (28, 29), "final.write": (29, 3),
-       "obs.rebuild": (5, 30), "obs.barrier": (30, 31), "obs.write": (31, 6)}
+       "obs.rebuild": (5, 30), "obs.barrier": (30, 31), "obs.write": (31, 6),
+       "q.env_step": (1, 22), "q.outputs": (22, 23), "bo.setup": (23, 19), "bo.channels": (19, 20),
+       "bo.finish_nsd": (20, 21)}
 CASES = {"cfg2": (4096, dict(random_map_width=3, random_map_height=3)),
          "cfg5": (131072, dict(random_map_width=5, random_map_height=5)),
          "cfg4": (262144, dict(random_map_width=3, random_map_height=3)),
@@ -63,7 +65,7 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
     lo, hi = st[:, 0], st[:, 6]
     out = {}
     for n, (a, b) in SUB.items():
-        if n.startswith("traf."):  # k_traffic (after k_env; 64-lane workgroups share the slot rows)
+        if n.startswith("traf.") and spread:  # k_traffic (after k_env; 64-lane workgroups share the slot rows)
             ok = (st[:, a] > 0) & (st[:, b] >= st[:, a]) & (st[:, b] - st[:, a] < 1e9)
         else:
             ok = (st[:, a] >= lo) & (st[:, a] <= hi) & (st[:, b] >= st[:, a]) & (st[:, b] <= hi)
