@@ -2823,6 +2823,19 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
     Lds best = shrink(lds_layout(c, envs));
     while (best.envs > 16 && lds_bytes(best) + sizeof(Tables) > 80 * 1024) best = shrink(lds_layout(c, best.envs / 2));
     if (lds_bytes(best) + sizeof(Tables) > 80 * 1024) best = shrink(lds_layout(c, envs));
+    // Batches that fill every CU with 256 envs: one workgroup per CU with 64 env lanes in each of
+    // its four waves (one wave per SIMD, the observation image sub-batched to fit) instead of two
+    // workgroups of 128 envs (two half-filled waves per SIMD): the car pass issues half as many
+    // instructions per env.  configs[2] (65 536 envs): k_env<true> + k_traffic 1 405 -> 1 283 us.
+    // (Two workgroups of two waves each land on three SIMDs, tools/micro/hwid2.hip.)
+    if ((h->tune_epb == 0 && n_envs >= (uint64_t)256 * kBlock) || h->tune_epb == kBlock) {
+      Lds l = lds_layout(c, kBlock);
+      while (l.sub_envs > 8 && lds_bytes(l) + sizeof(Tables) > 160 * 1024) {
+        l.sub_envs /= 2;
+        l.stream_words = img_words(l.sub_envs, l.seg_bits);
+      }
+      if (lds_bytes(l) + sizeof(Tables) <= 160 * 1024) best = l;
+    }
     h->L = best;
   }
   if (!c.need_car && h->L.envs == kBlock) {

@@ -131,16 +131,16 @@ def test_sharded_batch_equals_the_global_batch():
 
 
 @pytest.mark.parametrize("n,kw,want", [
-    (65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5), 2),  # configs[2]
-    (131072, dict(random_map_width=5, random_map_height=5), 4),                       # configs[4] shard
-    (262144, dict(random_map_width=3, random_map_height=3), 4),                       # configs[3]
+    (65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5), 256),  # configs[2]
+    (1048576, dict(random_map_width=5, random_map_height=5), 512),                      # configs[4]
+    (262144, dict(random_map_width=3, random_map_height=3), 1024),                      # configs[3]
 ])
 def test_step_kernel_occupancy(n, kw, want):
-    """The LDS sizing of the bench workloads keeps the intended workgroups per CU resident (a few
-    bytes over the budget once halved cfg3's throughput: one traffic workgroup per CU)."""
+    """The LDS sizing of the bench workloads keeps the intended env lanes per CU resident (envs per
+    workgroup x resident workgroups; a few bytes over the budget once halved cfg3's throughput)."""
     from pgtg_amd.vector import PGTGVecEnv
     vec = PGTGVecEnv(n, spec=_spec(**kw))
     try:
-        assert vec.occupancy() >= want, (vec.launch_info(), vec.occupancy())
+        assert vec.launch_info()[0] * vec.occupancy() >= want, (vec.launch_info(), vec.occupancy())
     finally:
         vec.close()
