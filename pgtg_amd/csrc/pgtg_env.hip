@@ -1226,10 +1226,11 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
     if (!(a & kCarEmpty)) {
       const int x = (int)(a & 255u), y = (int)((a >> 8) & 255u), prof = (int)((a >> 21) & 7u);
       int route = (int)((a >> 16) & 31u), delay = (int)((a >> 24) & 3u);
-      // ---- map lookups (no draws)
+      // ---- map lookups (no draws).  Every LDS read is unconditional at a valid index (a conditional
+      // read is a branch the compiler cannot hoist the read out of, and each one waited alone); the
+      // reads of one level go out together.
       const int tx = x / kTile, ty = y / kTile, lx = x - tx * kTile, ly = y - ty * kTile;
       const int t0 = ty * tw + tx, sq = lx * 9 + ly;
-      const int s_old = t0 * 32 + sT.li[plan_exits(pl[t0])][sq];
       // neighbours up, down, left, right (_get_next_car_position_and_route's order)
       const bool ok0 = !(ly == 0 && ty == 0), ok1 = !(ly == 8 && ty == th - 1);
       const bool ok2 = !(lx == 0 && tx == 0), ok3 = !(lx == 8 && tx == tw - 1);
@@ -1237,11 +1238,20 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       const int nt2 = lx == 0 ? t0 - 1 : t0, nt3 = lx == 8 ? t0 + 1 : t0;
       const int nq0 = ly == 0 ? sq + 8 : sq - 1, nq1 = ly == 8 ? sq - 8 : sq + 1;
       const int nq2 = lx == 0 ? sq + 72 : sq - 9, nq3 = lx == 8 ? sq - 72 : sq + 9;
-      const uint32_t e0 = ok0 ? plan_exits(pl[nt0]) : 0u, e1 = ok1 ? plan_exits(pl[nt1]) : 0u;
-      const uint32_t e2 = ok2 ? plan_exits(pl[nt2]) : 0u, e3 = ok3 ? plan_exits(pl[nt3]) : 0u;
-      const uint32_t l0 = e0 ? sT.lanes[e0][nq0] : 0u, l1 = e1 ? sT.lanes[e1][nq1] : 0u;
-      const uint32_t l2 = e2 ? sT.lanes[e2][nq2] : 0u, l3 = e3 ? sT.lanes[e3][nq3] : 0u;
+      const uint32_t p0 = pl[t0];
+      const uint32_t pn0 = pl[ok0 ? nt0 : t0], pn1 = pl[ok1 ? nt1 : t0];
+      const uint32_t pn2 = pl[ok2 ? nt2 : t0], pn3 = pl[ok3 ? nt3 : t0];
       const uint32_t rtl = *reinterpret_cast<const uint32_t*>(sT.route_type_lane[route]);
+      // this car's behaviour thresholds (environment.py:64-109), read up front
+      const uint64_t th_delay = sT.beh_t[BEH_DELAY][prof], th_speed = sT.beh_t[BEH_SPEED][prof];
+      const uint64_t th_yellow = sT.beh_t[BEH_YELLOW][prof], th_red = sT.beh_t[BEH_RED][prof];
+      const uint64_t th_go = sT.beh_t[BEH_GO][prof];
+      const int b_mf = sT.beh_mf[prof], b_pt = sT.beh_pt[prof];
+      const uint32_t e0 = ok0 ? plan_exits(pn0) : 0u, e1 = ok1 ? plan_exits(pn1) : 0u;
+      const uint32_t e2 = ok2 ? plan_exits(pn2) : 0u, e3 = ok3 ? plan_exits(pn3) : 0u;
+      const int s_old = t0 * 32 + sT.li[plan_exits(p0)][sq];
+      const uint32_t l0 = sT.lanes[e0][nq0], l1 = sT.lanes[e1][nq1];  // row 0 (no exits) is empty
+      const uint32_t l2 = sT.lanes[e2][nq2], l3 = sT.lanes[e3][nq3];
       int dec = -1;
       bool dec_all = false;
 #pragma unroll
@@ -1258,19 +1268,23 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       const int dk = dec < 0 ? 0 : dec;
       const int tg_t = sel4(dk, nt0, nt1, nt2, nt3), tg_q = sel4(dk, nq0, nq1, nq2, nq3);
       const uint32_t tg_ln = sel4(dk, l0, l1, l2, l3);
-      const uint32_t p_tg = pl[dec < 0 ? t0 : tg_t];
+      const uint32_t p_tg = dec < 0 ? p0 : sel4(dk, pn0, pn1, pn2, pn3);  // pl[tg_t] (read above)
       const uint32_t ex_tg = plan_exits(p_tg);
-      const bool tl = plan_otype(p_tg) == 4u && !bit81(sT.wall[ex_tg], tg_q) && bit81(sT.obst[plan_omask(p_tg)], tg_q);
-      const int s_tg = tg_t * 32 + sT.li[ex_tg][tg_q];
-      const int occ_tg = dec < 0 ? 0 : occ_get(occ, s_tg);
+      const uint32_t wall_tg = bit81(sT.wall[ex_tg], dec < 0 ? sq : tg_q);
+      const uint32_t obst_tg = bit81(sT.obst[min(plan_omask(p_tg), (uint32_t)PGTG_N_OBST_MASKS - 1u)], dec < 0 ? sq : tg_q);
+      const bool tl = plan_otype(p_tg) == 4u && !wall_tg && obst_tg;
+      const int li_tg = sT.li[ex_tg][tg_q];
+      const int s_tg = dec < 0 ? s_old : tg_t * 32 + li_tg;
+      const int occ_raw = occ_get(occ, s_tg);
+      const int occ_tg = dec < 0 ? 0 : occ_raw;
       // ---- draws (_should_car_move, route choice / light / following, _spawn_new_car)
       const bool act = delay == 0;
       bool delayed = false, move = false;
       if (act) {
-        delayed = pcg_draw(cr, false, 0u) < sT.beh_t[BEH_DELAY][prof];
+        delayed = pcg_draw(cr, false, 0u) < th_delay;
         const uint64_t r2 = pcg_draw(cr, delayed, 3u);
         if (delayed) delay = 1 + (int)r2;  // integers(1, 4)
-        else move = r2 < sT.beh_t[BEH_SPEED][prof];
+        else move = r2 < th_speed;
       } else {
         delay -= 1;
       }
@@ -1282,11 +1296,11 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       const uint32_t s3_n = kind == 1 ? nr_all : nsp;
       uint64_t r3 = 0;
       if ((kind == 1 || kind == 3 || lit) && !(s3_int && s3_n <= 1u)) r3 = pcg_draw(cr, s3_int, s3_n);
-      const bool stop = lit && (color == 1 ? r3 < sT.beh_t[BEH_YELLOW][prof] : !(r3 < sT.beh_t[BEH_RED][prof]));
-      const bool go_try = kind == 2 && !stop && occ_tg > 0 && (sT.beh_mf[prof] == 0 || (int)pat > sT.beh_pt[prof]);
+      const bool stop = lit && (color == 1 ? r3 < th_yellow : !(r3 < th_red));
+      const bool go_try = kind == 2 && !stop && occ_tg > 0 && (b_mf == 0 || (int)pat > b_pt);
       uint64_t r4 = 0;
       if (go_try || kind == 3) r4 = pcg_draw(cr, false, 0u);
-      const bool leaves = kind == 3 || kind == 1 || (kind == 2 && !stop && (occ_tg == 0 || (go_try && r4 < sT.beh_t[BEH_GO][prof])));
+      const bool leaves = kind == 3 || kind == 1 || (kind == 2 && !stop && (occ_tg == 0 || (go_try && r4 < th_go)));
       if (leaves) {  // the car's square loses it
         if (sat && occ_get(occ, s_old) >= kOccMax) {
           // exact recount from HBM (this car's slot still holds its old square)
