@@ -196,8 +196,10 @@ __device__ __forceinline__ uint32_t square_flags(const DevCfg& c, const Plan& pl
     if ((int)(v.sg & 0xffu) == t && (int)((v.sg >> 8) & 0xffu) == d) f |= SQ_START;
     if ((int)((v.sg >> 16) & 0xffu) == t && (int)(v.sg >> 24) == d) f |= SQ_FINAL;
   }
+  // (read unconditionally, at a valid row: a conditional LDS read is a branch waited on alone)
+  const uint32_t ob = bit81(sT.obst[min(plan_omask(p), (uint32_t)PGTG_N_OBST_MASKS - 1u)], sq);
   uint32_t ot = plan_otype(p);
-  if (ot && !wall && bit81(sT.obst[plan_omask(p)], sq)) f |= SQ_ICE << (ot - 1);
+  if (ot && !wall && ob) f |= SQ_ICE << (ot - 1);
   return f;
 }
 __device__ __forceinline__ uint32_t square_lanes(const DevCfg& c, const Plan& pl, int x, int y) {
@@ -1050,13 +1052,21 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
         }
       }
     }
+    // every table row read unconditionally at a valid index, then selected (conditional LDS reads
+    // are branches whose reads are waited on one at a time)
+    const bool sg_on = sd >= 0 && ((ex >> sd) & 1u), fi_on = t == gl_t && ((ex >> gl_d) & 1u);
+    const bool st_on = t == st_t && ((ex >> st_d) & 1u);
+    const uint32_t om = min(plan_omask(p), (uint32_t)PGTG_N_OBST_MASKS - 1u);
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       W3[k] = sT.wall[ex][k];
-      if (sd >= 0 && ((ex >> sd) & 1u)) (used ? US : SG)[k] = sT.seg[sd][k];
-      if (t == gl_t && ((ex >> gl_d) & 1u)) FI[k] = sT.seg[gl_d][k];
-      if (t == st_t && ((ex >> st_d) & 1u)) ST[k] = sT.seg[st_d][k];
-      if (ot) OB[k] = sT.obst[plan_omask(p)][k] & ~W3[k];
+      const uint32_t sgk = sT.seg[sd >= 0 ? sd : 0][k], fik = sT.seg[gl_d & 3][k], stk = sT.seg[st_d & 3][k];
+      const uint32_t obk = sT.obst[om][k];
+      US[k] = sg_on && used ? sgk : 0u;
+      SG[k] = sg_on && !used ? sgk : 0u;
+      FI[k] = fi_on ? fik : 0u;
+      ST[k] = st_on ? stk : 0u;
+      OB[k] = ot ? (obk & ~W3[k]) : 0u;
     }
     STAMP(19);
     for (int ci = 0; ci < c.n_channels; ci++) {
@@ -1807,8 +1817,10 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   TrafState ts{0, 0, 0, 0};
   bool occ_sat = false;  // a 4-bit occupancy counter saturated this launch (exact recounts from then on)
   int err = 0;
+  int act = 0;
   if (live) {
     v = rec_load(S.rec, i);
+    if (mode == MODE_STEP) act = actions[i];  // issued with the staging loads, not on the step's chain
     if ((TR && c.need_car)) {
       uint4 tr4 = S.traf[i];
       ts.n_cars = tr4.x & 0xffffu;
@@ -1855,7 +1867,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (live) {
     if (mode == MODE_STEP) {
       StepResult res{0.0, 0.0, 0u};
-      if (!err) err = env_step<TR>(c, S, i, v, pl, actions[i], res, occ, occ_sat, sp_l, ts, hist);
+      if (!err) err = env_step<TR>(c, S, i, v, pl, act, res, occ, occ_sat, sp_l, ts, hist);
       const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
       if (out.reward) out.reward[i] = res.reward;
       if (out.cost) out.cost[i] = res.cost;
@@ -2116,9 +2128,11 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
 
   EnvView v{};
   uint32_t qs = 0;
+  int act = 0;
   if (live) {
     v = rec_load(S.rec, i);
     qs = S.qstate[i];
+    act = actions[i];  // issued with the staging loads, not on the step's chain
     stage_plan(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, pdw);
     xf[slot * L.scratch_dw] = v.spawn;
     xf[slot * L.scratch_dw + 1] = qs;
@@ -2192,7 +2206,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     StepResult res{0.0, 0.0, 0u};
     bool occ_sat = false;
     TrafState ts{0, 0, 0, 0};
-    err = env_step<false>(c, S, i, v, pl, actions[i], res, nullptr, occ_sat, nullptr, ts, nullptr);
+    err = env_step<false>(c, S, i, v, pl, act, res, nullptr, occ_sat, nullptr, ts, nullptr);
     STAMP(22);
     const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
     if (out.reward) out.reward[i] = res.reward;
