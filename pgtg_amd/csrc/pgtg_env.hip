@@ -229,13 +229,23 @@ __device__ __forceinline__ int phase_color(const DevCfg& c, uint32_t ph) {
 // ------------------------------------------------------------------------------------------------
 // traffic helpers: occupancy counters per lane square in LDS (tile t, lane slot li -> t*32 + li)
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ int lane_slot(const DevCfg& c, const Plan& pl, int x, int y) {
+// (both reads unconditional at valid indices, so that a batch of lookups goes out together)
+__device__ __forceinline__ int lane_slot_tw(int tw, const Plan& pl, int x, int y) {
   int tx = x / kTile, ty = y / kTile;
   int lx = x - tx * kTile, ly = y - ty * kTile;
-  int t = ty * c.tw + tx;
+  int t = ty * tw + tx;
   uint32_t ex = plan_exits(pl[t]);
-  int li = ex ? sT.li[ex][lx * 9 + ly] : 255;
+  const int li_raw = sT.li[ex][lx * 9 + ly];
+  const int li = ex ? li_raw : 255;
   return li == 255 ? -1 : t * 32 + li;
+}
+__device__ __forceinline__ int lane_slot(const DevCfg& c, const Plan& pl, int x, int y) {
+  return lane_slot_tw(c.tw, pl, x, y);
+}
+// A DevCfg field as a value the compiler cannot re-load inside a loop (see ProfileCdf).
+__device__ __forceinline__ int pinned(int x) {
+  __asm__ volatile("" : "+s"(x));
+  return x;
 }
 __device__ __forceinline__ bool square_tlight(const DevCfg& c, const Plan& pl, int x, int y) {
   int tx = x / kTile, ty = y / kTile;
@@ -270,6 +280,29 @@ __device__ __forceinline__ int occ_at(const DevCfg& c, const Plan& pl, const uin
 __device__ __forceinline__ int kth_bit(uint32_t m, int k) {
   for (int j = 0; j < k; j++) m &= m - 1u;
   return __ffs((int)m) - 1;
+}
+
+// The driver-profile CDF thresholds as values the compiler cannot re-load from the handle's
+// DevCfg: under scalar-register pressure it rematerialises such loop-invariant loads inside the car
+// loops, and every re-load is a scalar-cache round trip the loop then waits for.
+struct ProfileCdf {
+  uint64_t t[4];
+};
+__device__ __forceinline__ ProfileCdf pin_profile_cdf(const DevCfg& c) {
+  ProfileCdf p;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    uint64_t x = c.profile_t[j];
+    __asm__ volatile("" : "+s"(x));
+    p.t[j] = x;
+  }
+  return p;
+}
+__device__ __forceinline__ int profile_of(const ProfileCdf& p, uint64_t u) {
+  int prof = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) prof += (u < p.t[j]) ? 0 : 1;
+  return prof;
 }
 
 constexpr uint32_t kCarEmpty = 1u << 31;  // w0 of a slot without a car
@@ -808,6 +841,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
     STAMP(26);  // (slot shared with k_env's removal-loop record: k_traffic runs later)
     if (sub != 0) return 0;
     // the cars in id order: profile and route draws -> slots 0 .. k-1
+    const ProfileCdf pcdf = pin_profile_cdf(c);
     uint64_t a_m = cs.at(0);  // slot index, advanced by the env stride
     for (int m = 0; m < k; m++) {
       const uint32_t code = out[m];
@@ -820,9 +854,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
       const uint32_t nr = __popc(rl);
       if (nr == 0) return PGTG_E_MAP;  // "a car was spawned on a field where no car lane was found"
       const uint64_t u = pcg_draw(cr, false, 0u);
-      int prof = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) prof += (u < c.profile_t[j]) ? 0 : 1;
+      const int prof = profile_of(pcdf, u);
       const uint32_t rk = nr > 1u ? (uint32_t)pcg_draw(cr, true, nr) : 0u;
       const int route = sT.lane_route[kth_bit(rl, (int)rk)];
       cs.w0[a_m] = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
@@ -1218,6 +1250,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
   // (wave-uniform: packing is right for any list, and a uniform flag keeps the loop free of
   // exec-mask juggling around the packing writes)
   const bool pack = __any(tail0 > (int)ts.n_cars + kCompactSlack);
+  const ProfileCdf pcdf = pin_profile_cdf(c);
   int t_out = tail0, w = 0;
   const uint64_t nst = S.n;
   // software pipeline: the next slot's words are requested before the current car is processed, so
@@ -1329,9 +1362,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
         }
         const uint32_t rl = square_lanes(c, pl, sx, sy) & 0x0fffffffu;
         const uint32_t nr = __popc(rl);
-        int nprof = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) nprof += (r4 < c.profile_t[q]) ? 0 : 1;
+        const int nprof = profile_of(pcdf, r4);
         if (nr == 0) return PGTG_E_MAP;
         const uint32_t r5 = nr > 1u ? (uint32_t)pcg_draw(cr, true, nr) : 0u;
         const int nroute = sT.lane_route[kth_bit(rl, (int)r5)];
@@ -1837,17 +1868,21 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     // loads in flight per lane)
     for (int w = 0; w < c.nt * 4; w++) traf_w[w] = 0u;  // 16 B of 4-bit counters per tile
     const CarSlots cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
-    const int tail = (int)ts.tail;
+    const int tail = (int)ts.tail, tw = pinned(c.tw);
     for (int k0 = 0; k0 < tail; k0 += 16) {
       uint32_t a16[16];
 #pragma unroll
       for (int g = 0; g < 16; g++) a16[g] = cs.w0[cs.at(k0 + g < tail ? k0 + g : 0)];
+      // the 16 slot lookups first (every slot holds valid coordinates: empty slots read as (0, 0),
+      // slots past the tail as slot 0), their reads batched; then the counter updates in order
+      int sl[16];
+#pragma unroll
+      for (int g = 0; g < 16; g++) sl[g] = lane_slot_tw(tw, pl, (int)(a16[g] & 255u), (int)((a16[g] >> 8) & 255u));
 #pragma unroll
       for (int g = 0; g < 16; g++) {
         if (k0 + g < tail && !(a16[g] & kCarEmpty)) {
-          int sl = lane_slot(c, pl, (int)(a16[g] & 255u), (int)((a16[g] >> 8) & 255u));
-          if (sl < 0) err = PGTG_E_UNSUPPORTED;
-          else occ_inc(occ, sl, occ_sat);
+          if (sl[g] < 0) err = PGTG_E_UNSUPPORTED;
+          else occ_inc(occ, sl[g], occ_sat);
         }
       }
     }
