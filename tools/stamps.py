@@ -72,6 +72,10 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
         if ok.any():
             out[n] = (int((st[ok, b] - st[ok, a]).mean()), round(float(ok.mean()), 2))
     print("  sub-phases (mean cycles, fraction of waves):", out, flush=True)
+    if not spread:  # k_envq env waves: the observation channel loop's split (slots 24, 25)
+        okc = (st[:, 24] > 0) & (st[:, 24] < 1e7) & (st[:, 25] < 1e7)
+        if okc.any():
+            print("  channel loop: code+select", int(st[okc, 24].mean()), "bit sink", int(st[okc, 25].mean()), flush=True)
     # slot 26 is k_traffic's lookup stamp when there is traffic
     okr = (not spread) & (st[:, 14] >= lo) & (st[:, 14] <= hi) & (st[:, 27] > 0) & (st[:, 27] < 1000)
     if okr.any():
