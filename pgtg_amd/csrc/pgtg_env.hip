@@ -1040,14 +1040,18 @@ struct BitSink {
 
 // Observation of one env into the image at bit offset bit0 (see BitSink): channel by channel, each
 // the window's squares row-major over x, then y.
+// Channels [ch_lo, ch_hi) only (default all) when the lanes of a group share one env's image (the
+// group's sinks merge at their shared words); `head`: also the next-subgoal direction.
 template <bool TR>
 __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
-                                          uint32_t* img, uint32_t bit0, ObsInfo& oi, const uint8_t* occ) {
-  BitSink sink(img, bit0);
+                                          uint32_t* img, uint32_t bit0, ObsInfo& oi, const uint8_t* occ,
+                                          int ch_lo = 0, int ch_hi = -1, bool head = true) {
+  const int WW = c.win * c.win;
+  if (ch_hi < 0) ch_hi = c.n_channels;
+  BitSink sink(img, bit0 + (uint32_t)(ch_lo * WW));
   int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
   int tx = pix / kTile, ty = piy / kTile;
   int color = phase_color(c, v.phase);
-  const int WW = c.win * c.win;
   if (!c.sliding) {
     oi.x0 = tx * kTile;
     oi.y0 = ty * kTile;
@@ -1101,7 +1105,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
       OB[k] = ot ? (obk & ~W3[k]) : 0u;
     }
     STAMP(19);
-    for (int ci = 0; ci < c.n_channels; ci++) {
+    for (int ci = ch_lo; ci < ch_hi; ci++) {
       int code = c.channels[ci];
       uint32_t out3[3];
 #pragma unroll
@@ -1131,7 +1135,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
     }
   } else {
     const int win = c.win;
-    for (int ci = 0; ci < c.n_channels; ci++) {
+    for (int ci = ch_lo; ci < ch_hi; ci++) {
       int code = c.channels[ci];
       for (int w0 = 0; w0 < WW; w0 += 32) {
         uint32_t acc = 0;
@@ -1168,7 +1172,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
   STAMP(20);
   sink.finish();
   oi.nsd = -1;
-  if (c.next_subgoal) {
+  if (c.next_subgoal && head) {
     int t = ty * c.tw + tx;
     int sd = plan_sgdir(pl[t]);
     int gl_t = (int)((v.sg >> 16) & 0xffu);
@@ -2136,6 +2140,41 @@ __device__ __forceinline__ void sub_barrier(uint32_t* ctr, uint32_t target) {
 // write the terminal observations, take queued maps for the envs that finished and write the new
 // observations, synchronising among themselves only.  Only when some env's ring is empty (the
 // first step after a reset, or a refill carried over) do they wait for the head refills.
+// The map-queue step's observation images.  With <= 32 envs per workgroup they all sit in wave 0
+// and most of its lanes are idle, so each env's image is built by a group of G = 64 / E lanes (up to
+// 4): lane e (the env's own) and lanes e + E, e + 2E, ... take a quarter of the channels each (their
+// bit sinks merge at the shared words), the env's lane also the next-subgoal direction.  `want`:
+// this lane's env needs an image.  Otherwise every env lane builds its own.
+__device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, const EnvView& v, bool want,
+                                          uint32_t* st, ObsInfo& oi, const Lds& L, int wave, int lane) {
+  const int E = L.envs;
+  if (E <= 32) {
+    if (wave != 0) return;
+    const int G = 64 / E, e = lane & (E - 1), sub = lane / E;
+    EnvView ve{};
+    ve.px = __shfl(v.px, e);
+    ve.py = __shfl(v.py, e);
+    ve.sg = (uint32_t)__shfl((int)v.sg, e);
+    ve.phase = (uint32_t)__shfl((int)v.phase, e);
+    ve.used = (uint64_t)(uint32_t)__shfl((int)(uint32_t)v.used, e) |
+              (uint64_t)(uint32_t)__shfl((int)(uint32_t)(v.used >> 32), e) << 32;
+    const int w_e = __shfl(want ? 1 : 0, e);
+    if (!w_e) return;
+    const int C = c.n_channels;
+    extern __shared__ uint32_t lds[];
+    const Plan pl{reinterpret_cast<uint16_t*>(lds + e * L.plan_stride_dw)};
+    build_obs<false>(c, S, pl, ve, st, (uint32_t)e * (uint32_t)c.obs_bytes, oi, nullptr, sub * C / G,
+                     (sub + 1) * C / G, sub == 0);
+    return;
+  }
+  if (want) {
+    extern __shared__ uint32_t lds[];
+    const int slot = (int)threadIdx.x;
+    const Plan pl{reinterpret_cast<uint16_t*>(lds + slot * L.plan_stride_dw)};
+    build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
+  }
+}
+
 __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
                                                     DevState S, const uint8_t* __restrict__ actions, PgtgOutputs out,
                                                     Lds L) {
@@ -2251,13 +2290,13 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     if (out.braking) out.braking[i] = 0;
     my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
     if (lm && my_sel && out.final_obs) mark_lines(lm, out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)slot, (uint32_t)c.obs_bytes);
-    ObsInfo oi;  // the post-step image of every env (terminal for the finished ones)
     STAMP(23);
-    build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
-#ifdef PGTG_TUNING
-    if (L.diag == 9) build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);  // diagnostic
-#endif
-    write_small_outputs(c, out, i, v, oi, my_sel == 1);
+  }
+  // the post-step image of every env (terminal for the finished ones)
+  {
+    ObsInfo oi;
+    group_obs(c, S, v, live, st, oi, L, wave, lane);
+    if (live) write_small_outputs(c, out, i, v, oi, my_sel == 1);
   }
   if (env_wave) sel[slot] = my_sel;
   const uint64_t rm = __ballot(my_sel == 1);
@@ -2331,10 +2370,10 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     S.qstate[i] = (uint8_t)(nq | nh << 2);
   }
   STAMP(5);
-  if (reset_now) {
+  {
     ObsInfo oi;
-    build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
-    write_small_outputs(c, out, i, v, oi, false);
+    group_obs(c, S, v, reset_now, st, oi, L, wave, lane);
+    if (reset_now) write_small_outputs(c, out, i, v, oi, false);
   }
   STAMP(30);
   sub_barrier(ctr, 3u * np);
