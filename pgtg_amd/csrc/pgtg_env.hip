@@ -432,11 +432,12 @@ __device__ __forceinline__ bool still_connected(M hN, M hE, M hS, M hW, int w, i
 // still share an intact 4-cycle cannot disconnect anything; otherwise still_connected decides.
 template <typename M, int NW>
 __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, int gl_t, M& hN, M& hE, M& hS, M& hW) {
-  const int w = c.tw;
+  // (pinned: re-loaded from the DevCfg in the loop under scalar-register pressure otherwise)
+  const int w = pinned(c.tw), keep = pinned(c.keep), n_edges = pinned(c.n_edges);
   EdgeBits<NW> L;
-  L.init(c.n_edges);
-  int nrem = c.n_edges, count = c.n_edges;
-  if (!(count > c.keep && nrem > 0)) return;
+  L.init(n_edges);
+  int nrem = n_edges, count = n_edges;
+  if (!(count > keep && nrem > 0)) return;
   // The candidate sequence (draw -> list index -> edge pair) does not depend on whether earlier
   // removals were undone, so the next candidate is drawn while the current one is tested (two
   // independent dependency chains per iteration); the speculative draw is rolled back on exit.
@@ -489,7 +490,7 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, 
     dbg_bfs += __builtin_amdgcn_s_memtime() - tb0;
     dbg_iters++;
 #endif
-    if (!(count > c.keep && more)) {
+    if (!(count > keep && more)) {
       r = r_before;  // the reference stops drawing here
       break;
     }
