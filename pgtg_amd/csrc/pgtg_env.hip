@@ -1523,52 +1523,62 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
   int prev_minor = 0;
   const int gl_t = (int)((v.sg >> 16) & 0xffu), gl_d = (int)(v.sg >> 24);
   const int color = phase_color(c, v.phase);
+  // the subgoal reward of this episode's path (one read for every subgoal the step may cross)
+  const double ind_pl = sT.ind[v.path_len];
   for (int k = 0; k <= n; k++) {
+    // part k (the move to the next square) first: it does not depend on this square, so both
+    // squares' lookups go out together (unconditional reads at clamped coordinates)
+    int pxp = 0, pyp = 0;
+    if (k < n) {
+      const int ii = k + 1;
+      int minor = 0;
+      if (dx != 0 && dy != 0) {
+        double t = (double)ii * m;
+        t = t + 0.5;
+        minor = (int)floor(t);
+      }
+      if (xmajor) {
+        pxp = smaj;
+        pyp = (dy == 0) ? 0 : minor - prev_minor;
+      } else {
+        pyp = smaj;
+        pxp = (dx == 0) ? 0 : minor - prev_minor;
+      }
+      prev_minor = minor;
+    }
+    const int nx = cx + pxp, ny = cy + pyp;
+    const int ccx = min(max(cx, 0), c.W - 1), ccy = min(max(cy, 0), c.H - 1);
+    const int cnx = min(max(nx, 0), c.W - 1), cny = min(max(ny, 0), c.H - 1);
+    const uint32_t f_here = square_flags(c, pl, v, ccx, ccy);
+    const uint32_t f_next = square_flags(c, pl, v, cnx, cny);
+    int occ_here = 0;
+    if (TR && c.need_car) occ_here = occ_at(c, pl, occ, ccx, ccy);
     // crash: outside, wall (cars: traffic pass)
     if (!inside(c, cx, cy)) {
       if (c.separate_cost) cost += c.crash_penalty; else reward -= c.crash_penalty;
       v.flags |= kFlagTerminated;
       break;
     }
-    uint32_t f = square_flags(c, pl, v, cx, cy);
-    if ((f & SQ_WALL) || ((TR && c.need_car) && !c.ignore_collisions && occ_at(c, pl, occ, cx, cy) > 0)) {
+    const uint32_t f = f_here;
+    if ((f & SQ_WALL) || ((TR && c.need_car) && !c.ignore_collisions && occ_here > 0)) {
       if (c.separate_cost) cost += c.crash_penalty; else reward -= c.crash_penalty;
       v.flags |= kFlagTerminated;
       break;
     }
     if (f & SQ_FINAL) {
-      double add = sT.ind[v.path_len] + c.final_goal_bonus;
+      double add = ind_pl + c.final_goal_bonus;
       if (c.separate_cost) perf += add; else reward += add;
       v.flags |= kFlagTerminated;
       break;
     }
     if (f & SQ_SUBGOAL) {
-      if (c.separate_cost) perf += sT.ind[v.path_len]; else reward += sT.ind[v.path_len];
+      if (c.separate_cost) perf += ind_pl; else reward += ind_pl;
       // set_subgoals_to_used: the flood fill covers exactly this tile's subgoal segment
       v.used |= 1ull << ((cy / kTile) * c.tw + cx / kTile);
     }
     if (k == n) break;
-    // part k
-    int ii = k + 1, pxp, pyp;
-    int minor = 0;
-    if (dx == 0 || dy == 0) {
-      minor = 0;
-    } else {
-      double t = (double)ii * m;
-      t = t + 0.5;
-      minor = (int)floor(t);
-    }
-    if (xmajor) {
-      pxp = smaj;
-      pyp = (dy == 0) ? 0 : minor - prev_minor;
-    } else {
-      pyp = smaj;
-      pxp = (dx == 0) ? 0 : minor - prev_minor;
-    }
-    prev_minor = minor;
     // red light at the next square (phase after this tick's increment)
-    int nx = cx + pxp, ny = cy + pyp;
-    if (color == 2 && inside(c, nx, ny) && (square_flags(c, pl, v, nx, ny) & SQ_TLIGHT)) {
+    if (color == 2 && inside(c, nx, ny) && (f_next & SQ_TLIGHT)) {
       if (c.separate_cost) cost += c.tl_penalty; else reward -= c.tl_penalty;
     }
     if (f & SQ_ICE) {
