@@ -254,6 +254,83 @@ __device__ __forceinline__ uint64_t pcg_draw(Pcg& g, bool is_int, uint32_t n) {
   return m >> 32;
 }
 
+// A PCG64 stream with its next 64-bit output computed one step ahead.  A draw takes the
+// precomputed output at once and computes the following one, which does not depend on what the
+// caller does with the draw, so the 128-bit multiply chain of a step overlaps the caller's work
+// instead of sitting between consecutive dependent draws.  `g` is the consumed state (with the
+// 32-bit buffer) -- what is stored back; identical outputs to Pcg's.
+struct PcgAhead {
+  Pcg g;
+  uint64_t shi_a, slo_a;  // step(g)
+  uint64_t out_a;         // its output: the next draw
+};
+__device__ __forceinline__ uint64_t pcg_output(uint64_t shi, uint64_t slo) {
+  const uint64_t x = shi ^ slo;
+  const unsigned rot = (unsigned)(shi >> 58);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+__device__ __forceinline__ PcgAhead ahead_init(const Pcg& g) {
+  PcgAhead a;
+  a.g = g;
+  Pcg t = g;
+  pcg_step(t);
+  a.shi_a = t.shi;
+  a.slo_a = t.slo;
+  a.out_a = pcg_output(t.shi, t.slo);
+  return a;
+}
+__device__ __forceinline__ uint64_t ahead_next64(PcgAhead& a) {
+  const uint64_t r = a.out_a;
+  a.g.shi = a.shi_a;
+  a.g.slo = a.slo_a;
+  Pcg t = a.g;
+  pcg_step(t);
+  a.shi_a = t.shi;
+  a.slo_a = t.slo;
+  a.out_a = pcg_output(t.shi, t.slo);
+  return r;
+}
+__device__ __forceinline__ uint32_t ahead_next32(PcgAhead& a) {
+  if (a.g.has) {
+    a.g.has = 0;
+    return a.g.buf;
+  }
+  const uint64_t v = ahead_next64(a);
+  a.g.has = 1;
+  a.g.buf = (uint32_t)(v >> 32);
+  return (uint32_t)v;
+}
+// pcg_draw / pcg_int on a PcgAhead (same draws, same order)
+__device__ __forceinline__ uint64_t ahead_draw(PcgAhead& a, bool is_int, uint32_t n) {
+  const bool step = !is_int || !a.g.has;
+  uint64_t v = 0;
+  if (step) v = ahead_next64(a);
+  if (!is_int) return v >> 11;
+  uint32_t r32;
+  if (step) {
+    r32 = (uint32_t)v;
+    a.g.has = 1;
+    a.g.buf = (uint32_t)(v >> 32);
+  } else {
+    r32 = a.g.buf;
+    a.g.has = 0;
+  }
+  uint64_t m = (uint64_t)r32 * n;
+  uint32_t left = (uint32_t)m;
+  if (left < n) {
+    const uint32_t thr = (0xffffffffu - (n - 1u)) % n;
+    while (left < thr) {
+      m = (uint64_t)ahead_next32(a) * n;
+      left = (uint32_t)m;
+    }
+  }
+  return m >> 32;
+}
+__device__ __forceinline__ uint32_t ahead_int(PcgAhead& a, uint32_t n) {
+  if (n <= 1u) return 0u;
+  return (uint32_t)ahead_draw(a, true, n);
+}
+
 // choice(k, p=p) with the host-normalised CDF (cumsum(p)/cumsum[-1]) as 53-bit thresholds:
 // searchsorted(u, 'right') counts the entries <= u
 template <int K>

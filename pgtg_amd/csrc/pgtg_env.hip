@@ -770,19 +770,21 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
       for (int w = 0; w < (np + 31) / 32; w++) seen[w] = 0u;
       STAMP(20);
       // Generator.choice(np, k, replace=False): Floyd's algorithm, then _shuffle_int
+      PcgAhead ca = ahead_init(cr);
       for (int j = np - k; j < np; j++) {
-        int val = (int)pcg_int(cr, (uint32_t)(j + 1));
+        int val = (int)ahead_int(ca, (uint32_t)(j + 1));
         if ((seen[val >> 5] >> (val & 31)) & 1u) val = j;
         seen[val >> 5] |= 1u << (val & 31);
         out[j - (np - k)] = (uint16_t)val;
       }
       STAMP(21);
       for (int m = k - 1; m >= 1; m--) {
-        int jj = (int)pcg_int(cr, (uint32_t)(m + 1));
+        int jj = (int)ahead_int(ca, (uint32_t)(m + 1));
         const uint16_t t = out[m], u = out[jj];
         out[m] = u;
         out[jj] = t;
       }
+      cr = ca.g;
     }
     wave_lds_sync();
     STAMP(22);
@@ -843,6 +845,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
     if (sub != 0) return 0;
     // the cars in id order: profile and route draws -> slots 0 .. k-1
     const ProfileCdf pcdf = pin_profile_cdf(c);
+    PcgAhead ca = ahead_init(cr);
     uint64_t a_m = cs.at(0);  // slot index, advanced by the env stride
     for (int m = 0; m < k; m++) {
       const uint32_t code = out[m];
@@ -854,15 +857,16 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
       const uint32_t rl = sT.lanes[ex_f][sq] & 0x0fffffffu;
       const uint32_t nr = __popc(rl);
       if (nr == 0) return PGTG_E_MAP;  // "a car was spawned on a field where no car lane was found"
-      const uint64_t u = pcg_draw(cr, false, 0u);
+      const uint64_t u = ahead_draw(ca, false, 0u);
       const int prof = profile_of(pcdf, u);
-      const uint32_t rk = nr > 1u ? (uint32_t)pcg_draw(cr, true, nr) : 0u;
+      const uint32_t rk = nr > 1u ? (uint32_t)ahead_draw(ca, true, nr) : 0u;
       const int route = sT.lane_route[kth_bit(rl, (int)rk)];
       cs.w0[a_m] = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
       cs.w1[a_m] = 0u;
       cs.id[a_m] = (uint32_t)m;
       a_m += N;
     }
+    cr = ca.g;
   }
   STAMP(23);
   ts.n_cars = (uint32_t)k;
@@ -1256,6 +1260,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
   // exec-mask juggling around the packing writes)
   const bool pack = __any(tail0 > (int)ts.n_cars + kCompactSlack);
   const ProfileCdf pcdf = pin_profile_cdf(c);
+  PcgAhead ca = ahead_init(cr);
   int t_out = tail0, w = 0;
   const uint64_t nst = S.n;
   // software pipeline: the next slot's words are requested before the current car is processed, so
@@ -1329,8 +1334,8 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       const bool act = delay == 0;
       bool delayed = false, move = false;
       if (act) {
-        delayed = pcg_draw(cr, false, 0u) < th_delay;
-        const uint64_t r2 = pcg_draw(cr, delayed, 3u);
+        delayed = ahead_draw(ca, false, 0u) < th_delay;
+        const uint64_t r2 = ahead_draw(ca, delayed, 3u);
         if (delayed) delay = 1 + (int)r2;  // integers(1, 4)
         else move = r2 < th_speed;
       } else {
@@ -1343,11 +1348,11 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       const bool s3_int = kind != 2;
       const uint32_t s3_n = kind == 1 ? nr_all : nsp;
       uint64_t r3 = 0;
-      if ((kind == 1 || kind == 3 || lit) && !(s3_int && s3_n <= 1u)) r3 = pcg_draw(cr, s3_int, s3_n);
+      if ((kind == 1 || kind == 3 || lit) && !(s3_int && s3_n <= 1u)) r3 = ahead_draw(ca, s3_int, s3_n);
       const bool stop = lit && (color == 1 ? r3 < th_yellow : !(r3 < th_red));
       const bool go_try = kind == 2 && !stop && occ_tg > 0 && (b_mf == 0 || (int)pat > b_pt);
       uint64_t r4 = 0;
-      if (go_try || kind == 3) r4 = pcg_draw(cr, false, 0u);
+      if (go_try || kind == 3) r4 = ahead_draw(ca, false, 0u);
       const bool leaves = kind == 3 || kind == 1 || (kind == 2 && !stop && (occ_tg == 0 || (go_try && r4 < th_go)));
       if (leaves) {  // the car's square loses it
         if (sat && occ_get(occ, s_old) >= kOccMax) {
@@ -1369,7 +1374,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
         const uint32_t nr = __popc(rl);
         const int nprof = profile_of(pcdf, r4);
         if (nr == 0) return PGTG_E_MAP;
-        const uint32_t r5 = nr > 1u ? (uint32_t)pcg_draw(cr, true, nr) : 0u;
+        const uint32_t r5 = nr > 1u ? (uint32_t)ahead_draw(ca, true, nr) : 0u;
         const int nroute = sT.lane_route[kth_bit(rl, (int)r5)];
         if (!pack) cs.w0[aw] = kCarEmpty;
         cs.w0[an] = (uint32_t)sx | (uint32_t)sy << 8 | (uint32_t)nroute << 16 | (uint32_t)nprof << 21;
@@ -1423,6 +1428,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
     }
     t_out = w + (t_out - tail0);
   }
+  cr = ca.g;
   ts.tail = (uint32_t)t_out;
   return 0;
 }
