@@ -1731,6 +1731,8 @@ struct Lds {
   int gen_off;         // k_envq: word offset of the helper lanes' plan scratch (kQueueLanes x plan_stride_dw)
   int lm_words;        // terminal-observation line mask words (0: test the selection bytes)
   int diag;            // diagnostic experiments (PGTG_DIAG; 0 in normal runs)
+  int stagger_ticks;   // first-round start offsets: workgroup b < stagger_wgs waits b/stagger_wgs of this (100 MHz ticks)
+  int stagger_wgs;     // workgroups resident in the first round (blocks per CU x CUs)
 };
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
 constexpr int kQueueDepth = 3;   // queued maps per env (a ring)
@@ -1760,6 +1762,8 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   // image and at least one wave without env slots
   l.queue = !c.need_car && c.n_rules == 0 && !c.fixed_map && envs <= kBlock - 64 && l.sub_envs >= envs;
   l.diag = 0;
+  l.stagger_ticks = 0;
+  l.stagger_wgs = 0;
 #ifdef PGTG_TUNING  // A/B and diagnostic builds only: the product library reads no environment
   if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);
   if (const char* e = getenv("PGTG_COMPACT")) l.compact = atoi(e);
@@ -1827,6 +1831,18 @@ __device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, con
 }
 
 // 4 waves per SIMD (<= 128 VGPRs) keeps 16 waves per CU resident to hide per-lane latency
+// Workgroups of one launch run the same phases (staging, step, terminal writes, reset, image writes)
+// and the first round starts them all at once, so the whole chip would write in the same windows
+// and compute in the same windows.  Offsetting the first round's starts along a ramp keeps the
+// offsets for every later round (a finishing workgroup's slot takes the next one at once), so the
+// write phases of some workgroups overlap the compute phases of others.
+__device__ __forceinline__ void stagger_start(const Lds& L) {
+  if (L.stagger_ticks <= 0 || blockIdx.x >= (unsigned)L.stagger_wgs) return;
+  const uint64_t wait = (uint64_t)L.stagger_ticks * blockIdx.x / (unsigned)L.stagger_wgs;
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < wait) __builtin_amdgcn_s_sleep(16);
+}
+
 template <bool TR>
 __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
                                                  DevState S, const uint8_t* __restrict__ actions,
@@ -1835,6 +1851,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   extern __shared__ uint32_t lds[];
   const DevCfg& c = *cfg;
   const int tid = threadIdx.x;
+  if (!TR) stagger_start(L);
   STAMP(0);
   // the traffic-reset list of the next launch starts empty (its previous consumer has finished)
   if ((TR && c.need_car) && mode != MODE_OBSERVE && blockIdx.x == 0 && tid == 0) S.tr_count[tr_slot ^ 1u] = 0u;
@@ -2198,6 +2215,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   extern __shared__ uint32_t lds[];
   const DevCfg& c = *cfg;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  stagger_start(L);
   STAMP(0);
   stage_tables(gtab, (int)(c.generic_channels ? sizeof(Tables) : offsetof(Tables, lanes)));
   const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
@@ -2331,16 +2349,23 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   if (reset_now) {  // the ring's head becomes the episode (env_reset without the generation)
     const uint4* q4 = reinterpret_cast<const uint4*>(S.qbuf + (i * kQueueDepth + qh) * (uint64_t)c.qrec_dw);
     uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
-    const int pwords = c.plan_stride / 2;
-    for (int k = 0; k < pwords / 4; k++) {
-      const uint4 w4 = q4[k];
-      dstp[k] = w4;
-      const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+    // all loads of the entry first: a load after a store to S.plan (which the compiler cannot
+    // tell apart from the queue) would wait for the one before it, one HBM latency per 16 bytes
+    const int nq = c.plan_stride / 8;  // 16-byte words of the tile plan (<= 8)
+    uint4 qw[8];
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (k * 4 + j < pdw) plan_w[k * 4 + j] = wv[j];
+    for (int k = 0; k < 8; k++) qw[k] = q4[k < nq ? k : 0];  // unconditional: registers, not scratch
+    const uint4 meta = q4[nq];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (k < nq) {
+        dstp[k] = qw[k];
+        const uint32_t wv[4] = {qw[k].x, qw[k].y, qw[k].z, qw[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (k * 4 + j < pdw) plan_w[k * 4 + j] = wv[j];
+      }
     }
-    const uint4 meta = q4[pwords / 4];
     const uint32_t k0 = v.spawn;
     if (c.need_ice || c.need_broken || c.need_sand) {
       SeedPool sp = ss_pool(S.seed[i]);
@@ -3008,6 +3033,21 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
     (void)hipFuncSetAttribute((const void*)k_env<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
     (void)hipFuncSetAttribute((const void*)k_env<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
     (void)hipFuncSetAttribute((const void*)k_envq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+  }
+  // first-round start offsets (stagger_start) for the launches without traffic
+  if (!c.need_car && c.n_rules == 0) {
+    int ncu = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || ncu < 1) ncu = 256;
+    const void* fn = h->L.queue ? (const void*)k_envq : (const void*)k_env<false>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, h->lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    h->L.stagger_wgs = ncu * per_cu;
+    // only launches of several rounds: one round has no later workgroups to keep the offsets
+    // (1 048 576 5x5 envs, 8 rounds: k_envq 476 -> 460 us; one round: slower)
+    const uint64_t blocks = (h->n + h->L.envs - 1) / h->L.envs;
+    h->L.stagger_ticks = blocks >= (uint64_t)3 * h->L.stagger_wgs ? 2500 : 0;
+#ifdef PGTG_TUNING
+    if (const char* e = getenv("PGTG_STAGGER")) h->L.stagger_ticks = atoi(e);
+#endif
   }
   return PGTG_OK;
 }

@@ -109,3 +109,24 @@ def test_random_config_parity(k):
                     assert np.array_equal(env.cars(int(i)), o.cars()), tag + " cars"
     finally:
         env.close()
+
+
+# Batches above the small-workgroup sizes: the 32/64/128/256-env layouts, the map queue and the
+# sub-batched observation pass under random feature combinations.  Every env at every step is
+# compared through the output digest (tests/test_gpu_exhaustive.py); traffic configurations are
+# capped at 40 000 envs to keep the restatement's share of the test in seconds.
+BIG = {  # fuzz seed: batch size
+    3: 12000, 7: 40000, 11: 140000, 17: 20000, 23: 70000, 29: 300000,
+}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("k", sorted(BIG))
+def test_random_config_every_env_large_batches(k):
+    from test_gpu_exhaustive import _compare, _spec
+    kw = random_kwargs(k)
+    n = BIG[k]
+    if kw["traffic_density"] > 0:
+        n = min(n, 40000)
+    # (few feature channels on small maps give few distinct observations)
+    _compare(_spec(kw), n, 10, None, f"fuzz {k} n={n} {kw}", min_distinct=200)

@@ -50,13 +50,13 @@ def _gpu_digests(spec, n, T, tune=None):
         env.close()
 
 
-def _compare(spec, n, T, tune=None, tag=""):
+def _compare(spec, n, T, tune=None, tag="", min_distinct=1000):
     got, kern, shape = _gpu_digests(spec, n, T, tune)
     ref = oracle.rollout_digest(spec, n, T, ACT_SEED)
     # the comparison has teeth: the rollout visits many distinct outputs.  Observations are local
     # 9x9 windows, so envs on small maps share digests (3x3 maps: 4 096 envs x 100 steps give 7 326
     # distinct ones, 262 144 x 20 give 13 072)
-    assert len(np.unique(ref)) >= min(ref.size // 4, 1000), "degenerate digests"
+    assert len(np.unique(ref)) >= min(ref.size // 4, min_distinct), "degenerate digests"
     bad = np.argwhere(got != ref)
     assert bad.size == 0, (f"{tag} {kern} {shape}: {len(bad)} (step, env) digests differ, first {bad[:8].tolist()}")
 

@@ -29,6 +29,7 @@ SUB = {"cars": (16, 17), "braking": (17, 18), "reset.seed": (8, 9), "reset.gener
        "bo.finish_nsd": (20, 21)}
 CASES = {"cfg2": (4096, dict(random_map_width=3, random_map_height=3)),
          "cfg5": (131072, dict(random_map_width=5, random_map_height=5)),
+         "cfg5big": (1048576, dict(random_map_width=5, random_map_height=5)),
          "cfg4": (262144, dict(random_map_width=3, random_map_height=3)),
          "cfg3": (65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5))}
 for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
