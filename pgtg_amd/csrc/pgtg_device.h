@@ -106,6 +106,10 @@ struct Tables {
   // north/west tile and d 1 (east) or 2 (south)
   uint32_t epk[kMaxEdges];
   uint8_t bt[kMaxBorder], bd[kMaxBorder];
+  // observation channel codes (DevCfg::channels as bytes): read per lane when the lanes of a group
+  // build different channels of one env's image (a per-lane index into the DevCfg block would be a
+  // dependent global load per channel)
+  uint8_t chan[PGTG_MAX_CHANNELS];
   uint32_t lanes[16][81];   // kLanes (copied only when traffic or lane/spawner channels need it)
   // traffic tables (copied with lanes): lane-square slot per square (255 = none), square per slot,
   // per-column masks (bit ly) of lane squares, lane-data spawners and the four "all" lanes

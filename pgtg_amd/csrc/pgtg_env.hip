@@ -1050,7 +1050,7 @@ struct BitSink {
 template <bool TR>
 __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
                                           uint32_t* img, uint32_t bit0, ObsInfo& oi, const uint8_t* occ,
-                                          int ch_lo = 0, int ch_hi = -1, bool head = true) {
+                                          int ch_lo = 0, int ch_hi = -1, bool head = true, bool lane_codes = false) {
   const int WW = c.win * c.win;
   if (ch_hi < 0) ch_hi = c.n_channels;
   BitSink sink(img, bit0 + (uint32_t)(ch_lo * WW));
@@ -1111,7 +1111,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
     }
     STAMP(19);
     for (int ci = ch_lo; ci < ch_hi; ci++) {
-      int code = c.channels[ci];
+      const int code = lane_codes ? (int)sT.chan[ci] : c.channels[ci];
       uint32_t out3[3];
 #pragma unroll
       for (int k = 0; k < 3; k++) {
@@ -1141,7 +1141,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
   } else {
     const int win = c.win;
     for (int ci = ch_lo; ci < ch_hi; ci++) {
-      int code = c.channels[ci];
+      const int code = lane_codes ? (int)sT.chan[ci] : c.channels[ci];
       for (int w0 = 0; w0 < WW; w0 += 32) {
         uint32_t acc = 0;
         if (code == PGTG_CH_TRAFFIC) {
@@ -2198,7 +2198,7 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
     extern __shared__ uint32_t lds[];
     const Plan pl{reinterpret_cast<uint16_t*>(lds + e * L.plan_stride_dw)};
     build_obs<false>(c, S, pl, ve, st, (uint32_t)e * (uint32_t)c.obs_bytes, oi, nullptr, sub * C / G,
-                     (sub + 1) * C / G, sub == 0);
+                     (sub + 1) * C / G, sub == 0, true);
     return;
   }
   if (want) {
@@ -3152,6 +3152,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     }
     memcpy(t.bt, c.bt, sizeof t.bt);
     memcpy(t.bd, c.bd, sizeof t.bd);
+    for (int k = 0; k < PGTG_MAX_CHANNELS; k++) t.chan[k] = (uint8_t)c.channels[k];
     memset(t.li, 255, sizeof t.li);
     memset(t.slot_sq, 255, sizeof t.slot_sq);
     for (int ex = 0; ex < 16; ex++) {
