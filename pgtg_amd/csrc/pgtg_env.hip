@@ -1196,6 +1196,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
 // step (pgtg/environment.py:1092-1281) for one lane; returns 0 or -code
 // ------------------------------------------------------------------------------------------------
 // ACTIONS_TO_ACCELERATION (pgtg/constants.py:6-16): action a -> (a/3 - 1, a%3 - 1)
+constexpr int kPathChunk = 4;  // agent path squares looked up together (env_step)
 __device__ __forceinline__ int acc_x(int a) { return a / 3 - 1; }
 __device__ __forceinline__ int acc_y(int a) { return a % 3 - 1; }
 
@@ -1531,7 +1532,77 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
   const int color = phase_color(c, v.phase);
   // the subgoal reward of this episode's path (one read for every subgoal the step may cross)
   const double ind_pl = sT.ind[v.path_len];
-  for (int k = 0; k <= n; k++) {
+  // Without obstacle effects or cars a step's path depends on the velocity alone, so the squares
+  // of kPathChunk parts are looked up together (one LDS latency per chunk instead of per part) and
+  // then walked in order.  A subgoal tile marked used earlier in the same step is tested against
+  // the updated mask (the lookups saw the step's initial one).
+  const bool chunked = !c.need_ice && !c.need_broken && !c.need_sand && !(TR && c.need_car);
+  for (int k0 = 0; chunked && k0 <= n; k0 += kPathChunk) {
+    int X[kPathChunk + 1], Y[kPathChunk + 1];
+    X[0] = cx;
+    Y[0] = cy;
+#pragma unroll
+    for (int j = 0; j < kPathChunk; j++) {  // part k0 + j: position k0 + j -> k0 + j + 1
+      int pxp = 0, pyp = 0;
+      if (k0 + j < n) {
+        int minor = 0;
+        if (dx != 0 && dy != 0) {
+          double t = (double)(k0 + j + 1) * m;
+          t = t + 0.5;
+          minor = (int)floor(t);
+        }
+        if (xmajor) {
+          pxp = smaj;
+          pyp = (dy == 0) ? 0 : minor - prev_minor;
+        } else {
+          pyp = smaj;
+          pxp = (dx == 0) ? 0 : minor - prev_minor;
+        }
+        prev_minor = minor;
+      }
+      X[j + 1] = X[j] + pxp;
+      Y[j + 1] = Y[j] + pyp;
+    }
+    uint32_t F[kPathChunk + 1];
+#pragma unroll
+    for (int j = 0; j <= kPathChunk; j++)
+      F[j] = square_flags(c, pl, v, min(max(X[j], 0), c.W - 1), min(max(Y[j], 0), c.H - 1));
+    bool go = true;
+#pragma unroll
+    for (int j = 0; j < kPathChunk; j++) {
+      if (go) {
+        const int k = k0 + j, x = X[j], y = Y[j];
+        const uint32_t f = F[j];
+        cx = x;
+        cy = y;
+        if (!inside(c, x, y) || (f & SQ_WALL)) {  // crash: outside, wall
+          if (c.separate_cost) cost += c.crash_penalty; else reward -= c.crash_penalty;
+          v.flags |= kFlagTerminated;
+          go = false;
+        } else if (f & SQ_FINAL) {
+          double add = ind_pl + c.final_goal_bonus;
+          if (c.separate_cost) perf += add; else reward += add;
+          v.flags |= kFlagTerminated;
+          go = false;
+        } else {
+          const int t = (y / kTile) * c.tw + x / kTile;
+          if ((f & SQ_SUBGOAL) && !((v.used >> t) & 1ull)) {
+            if (c.separate_cost) perf += ind_pl; else reward += ind_pl;
+            v.used |= 1ull << t;
+          }
+          if (k == n) {
+            go = false;
+          } else if (color == 2 && inside(c, X[j + 1], Y[j + 1]) && (F[j + 1] & SQ_TLIGHT)) {
+            if (c.separate_cost) cost += c.tl_penalty; else reward -= c.tl_penalty;
+          }
+        }
+      }
+    }
+    if (!go) break;
+    cx = X[kPathChunk];
+    cy = Y[kPathChunk];
+  }
+  for (int k = 0; !chunked && k <= n; k++) {
     // part k (the move to the next square) first: it does not depend on this square, so both
     // squares' lookups go out together (unconditional reads at clamped coordinates)
     int pxp = 0, pyp = 0;
