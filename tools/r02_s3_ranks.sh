@@ -12,4 +12,5 @@ for N in 2 4; do
     --master-addr 127.0.0.1 --master-port 2951$N bench.py --gpus $N --steps 40 --warmup 10 --digest $O/dg$N > $O/dg$N.json 2> $O/dg$N.err || exit 1
   python tools/digest_compare.py $O/dg1 $O/dg$N > $O/digest_compare_$N.json || exit 1
 done
+rm -f $O/*.npz  # 64 MB each: keep gpurun_out small enough to travel back
 cat $O/dg1.json $O/dg2.json $O/dg4.json $O/digest_compare_2.json $O/digest_compare_4.json
