@@ -2251,10 +2251,11 @@ __device__ __forceinline__ void sub_barrier(uint32_t* ctr, uint32_t target) {
 // bit sinks merge at the shared words), the env's lane also the next-subgoal direction.  `want`:
 // this lane's env needs an image.  Otherwise every env lane builds its own.
 __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, const EnvView& v, bool want,
-                                          uint32_t* st, ObsInfo& oi, const Lds& L, int wave, int lane) {
+                                          uint32_t* st, ObsInfo& oi, const Lds& L, int wave, int lane, bool post = true) {
   const int E = L.envs;
   if (E <= 32) {
     if (wave != 0) return;
+    STAMP(post ? 9 : 16);
     const int G = 64 / E, e = lane & (E - 1), sub = lane / E;
     EnvView ve{};
     ve.px = __shfl(v.px, e);
@@ -2265,11 +2266,13 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
               (uint64_t)(uint32_t)__shfl((int)(uint32_t)(v.used >> 32), e) << 32;
     const int w_e = __shfl(want ? 1 : 0, e);
     if (!w_e) return;
+    STAMP(post ? 10 : 17);
     const int C = c.n_channels;
     extern __shared__ uint32_t lds[];
     const Plan pl{reinterpret_cast<uint16_t*>(lds + e * L.plan_stride_dw)};
     build_obs<false>(c, S, pl, ve, st, (uint32_t)e * (uint32_t)c.obs_bytes, oi, nullptr, sub * C / G,
                      (sub + 1) * C / G, sub == 0, true);
+    STAMP(post ? 11 : 18);
     return;
   }
   if (want) {
@@ -2485,7 +2488,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   STAMP(5);
   {
     ObsInfo oi;
-    group_obs(c, S, v, reset_now, st, oi, L, wave, lane);
+    group_obs(c, S, v, reset_now, st, oi, L, wave, lane, false);
     if (reset_now) write_small_outputs(c, out, i, v, oi, false);
   }
   STAMP(30);
