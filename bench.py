@@ -108,7 +108,7 @@ def load_traffic(workload: str, n_envs: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--steps", type=int, default=1000)  # T >= 1000 after a 50-step warm-up
     ap.add_argument("--warmup", type=int, default=50)
     # Default: configs[4] (1 048 576 envs of 5x5 maps), the config BASELINE.json's metric is quoted
     # on, split over the N GPUs.  cfg2/cfg4/cfg3 = configs[1]/[3]/[2] (single-GPU configs).
