@@ -122,6 +122,7 @@ def main():
                     help="after the timed window, run --digest-steps more steps and save each rank's per-env "
                          "output digests to <path>.rank<r>.npz (tools/digest_compare.py)")
     ap.add_argument("--digest-steps", type=int, default=8)
+    ap.add_argument("--per-step", action="store_true", help="A/B: one pgtg_step host call per timed step")
     ap.add_argument("--envs-per-block", type=int, default=0, help="A/B: force the step kernel's envs per workgroup")
     args = ap.parse_args()
 
@@ -173,8 +174,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for t in range(args.warmup, args.warmup + args.steps):
-        env.step_actions(actions[t])
+    if args.per_step:
+        for t in range(args.warmup, args.warmup + args.steps):
+            env.step_actions(actions[t])
+    else:  # one host call queues the K launches (pgtg_step_many), same kernels and results
+        env.step_many(actions[args.warmup:args.warmup + args.steps])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -162,6 +162,11 @@ int pgtg_reset(pgtg_handle* h, const uint64_t* seeds_host, uint64_t seed_base, c
 int pgtg_reset_unseeded(pgtg_handle* h, const uint8_t* mask_dev);
 /* One tick for every env.  actions_dev: [N] uint8 in [0, 9). */
 int pgtg_step(pgtg_handle* h, const uint8_t* actions_dev);
+/* `ticks` consecutive pgtg_step calls from a resident rollout action buffer: tick k reads the [N]
+ * row at actions_dev + k * row_stride bytes (row_stride >= N).  Identical results to the loop of
+ * pgtg_step calls (the outputs hold the last tick's); one host call, so the launches are queued
+ * without per-tick host overhead.  Stops at the first launch error. */
+int pgtg_step_many(pgtg_handle* h, const uint8_t* actions_dev, uint64_t row_stride, uint64_t ticks);
 /* Fill [N] uint8 actions with a counter-based uniform hash of (seed, env_offset + env, t) --
  * synthetic rollouts; env_offset = global index of env 0 so that a sharded run draws the same
  * actions as one GPU running the whole batch. */

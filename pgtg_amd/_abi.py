@@ -28,7 +28,7 @@ PGTG_E_MAP = -5
 
 EXPORTED = [
     "pgtg_create", "pgtg_destroy", "pgtg_set_stream", "pgtg_set_outputs", "pgtg_reset",
-    "pgtg_reset_unseeded", "pgtg_step", "pgtg_random_actions", "pgtg_get_env_state", "pgtg_get_cars",
+    "pgtg_reset_unseeded", "pgtg_step", "pgtg_step_many", "pgtg_random_actions", "pgtg_get_env_state", "pgtg_get_cars",
     "pgtg_get_map_plan", "pgtg_get_squares", "pgtg_set_rules", "pgtg_set_agent", "pgtg_add_car", "pgtg_observe", "pgtg_get_counters",
     "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_launch_info", "pgtg_occupancy", "pgtg_step_kernel", "pgtg_last_error", "pgtg_enable_timing",
     "pgtg_timing_read", "pgtg_measure_hbm", "pgtg_state_size", "pgtg_dump_state", "pgtg_load_state",
@@ -111,6 +111,7 @@ def lib():
         "pgtg_reset": ([vp, vp, u64, vp], C.c_int),
         "pgtg_reset_unseeded": ([vp, vp], C.c_int),
         "pgtg_step": ([vp, vp], C.c_int),
+        "pgtg_step_many": ([vp, vp, u64, u64], C.c_int),
         "pgtg_random_actions": ([vp, vp, u64, u64, u64], C.c_int),
         "pgtg_measure_hbm": ([i32, u64, i32, C.POINTER(C.c_double)], C.c_int),
         "pgtg_state_size": ([vp, C.POINTER(u64)], C.c_int),

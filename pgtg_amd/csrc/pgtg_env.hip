@@ -3369,6 +3369,13 @@ int pgtg_step(pgtg_handle* h, const uint8_t* actions_dev) {
   return launch(h, actions_dev, nullptr, MODE_STEP);
 }
 
+int pgtg_step_many(pgtg_handle* h, const uint8_t* actions_dev, uint64_t row_stride, uint64_t ticks) {
+  if (!h || !actions_dev || row_stride < h->n) return PGTG_E_INVALID;
+  for (uint64_t k = 0; k < ticks; k++)
+    if (int rc = launch(h, actions_dev + k * row_stride, nullptr, MODE_STEP)) return rc;
+  return PGTG_OK;
+}
+
 int pgtg_observe(pgtg_handle* h) {
   if (!h) return PGTG_E_INVALID;
   return launch(h, nullptr, nullptr, MODE_OBSERVE);

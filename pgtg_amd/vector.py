@@ -205,6 +205,17 @@ class PGTGVecEnv:
         self._bind_stream()
         _check(self._lib.pgtg_step(self._h, C.c_void_p(actions_row.data_ptr())), self._h)
 
+    def step_many(self, actions):
+        """len(actions) ticks from a resident [T, N] uint8 device tensor in one host call
+        (include/pgtg.h pgtg_step_many); the outputs hold the last tick's."""
+        if actions.dim() != 2 or actions.shape[1] != self.num_envs or actions.dtype.itemsize != 1:
+            raise ValueError(f"expected a [T, {self.num_envs}] uint8 tensor, got {tuple(actions.shape)}")
+        if actions.device != self.device or actions.stride(1) != 1:
+            raise ValueError("actions must be a row-contiguous tensor on the env's device")
+        self._bind_stream()
+        _check(self._lib.pgtg_step_many(self._h, C.c_void_p(actions.data_ptr()), actions.stride(0),
+                                        actions.shape[0]), self._h)
+
     def observe(self):
         """Re-emit every env's observation (after set_agent / add_car)."""
         self._bind_stream()

@@ -207,3 +207,34 @@ def test_save_map_round_trip(tmp_path, seed):
             break
     env.close()
     fixed.close()
+
+
+@pytest.mark.parametrize("name", ["s3_queue", "traffic"])
+def test_step_many_equals_step_loop(name):
+    """pgtg_step_many (one host call for T ticks from a [T, N] buffer) == T pgtg_step calls: the
+    same digests after the last tick and on the ticks that follow."""
+    from pgtg_amd.digest import Digest
+    from pgtg_amd.vector import PGTGVecEnv
+    spec = _spec(CONFIGS[name])
+    n, k = 3000, 17  # odd k: the traffic handle's car-bank parity flips per launch
+    a, b = PGTGVecEnv(n, spec=spec, device=0), PGTGVecEnv(n, spec=spec, device=0)
+    try:
+        a.reset(seed=7)
+        b.reset(seed=7)
+        acts = a.random_actions(k, 0x5EED)
+        for t in range(k):
+            a.step_actions(acts[t])
+        b.step_many(acts)
+        da, db = Digest(a).step_digest().cpu().numpy(), Digest(b).step_digest().cpu().numpy()
+        assert np.array_equal(da, db), f"{name}: digests differ at {np.argwhere(da != db)[:5]}"
+        assert a.counters() == b.counters()
+        # the state blobs may differ in how far each handle's map-queue rings were filled ahead (a
+        # timing matter); what follows from the state must not: 8 more ticks on both
+        more = a.random_actions(8, 0x5EED, t0=k)
+        ra, rb = _rollout(a, Digest(a), more, 0, 8), _rollout(b, Digest(b), more, 0, 8)
+        assert np.array_equal(ra, rb), f"{name}: later ticks differ at {np.argwhere(ra != rb)[:5]}"
+        with pytest.raises(ValueError):
+            b.step_many(acts[0])
+    finally:
+        a.close()
+        b.close()

@@ -1,14 +1,21 @@
 #!/bin/bash
-# Round-2 GPU session 5: single-bank car store -- traffic parity (golden trajectories, exhaustive
-# cfg3, car-slot compaction, saturating counters), then cfg3 bench + kernel stats + PMC traffic.
-set -o pipefail
+# Round 2, last session: the GPU suite, smoke() and the default bench line on the final tree, then an
+# interleaved A/B of the timed loop (one pgtg_step host call per step vs one pgtg_step_many call).
 O=gpurun_out/r02s5
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_car_slots.py tests/test_gpu_parity.py tests/test_gpu_occupancy.py tests/test_gpu_traffic_groups.py "tests/test_gpu_exhaustive.py::test_cfg3_long_cautious_traffic" "tests/test_gpu_exhaustive.py::test_every_env_every_step[cfg3_all_65536x3]" "tests/test_gpu_exhaustive.py::test_every_env_every_step[sliding_traffic_6000]" tests/test_gpu_state.py tests/test_gpu_env.py > $O/pytest_traffic.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -5 $O/pytest_traffic.log
-[ $rc -eq 0 ] || exit 1
-timeout -k 10 300 python -u bench.py --workload cfg3 --steps 200 --warmup 20 --no-cpu-baseline > $O/b_cfg3.json || exit 1
-timeout -k 10 900 bash tools/gpu_profile.sh r02s5 cfg3 > $O/profile.log 2>&1; echo "profile rc=$?"
-cp -r gpurun_out/prof_r02s5 $O/ 2>/dev/null
-cat $O/b_cfg3.json
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+tail -2 $O/tests.log
+grep -q " passed" $O/tests.log && ! grep -q "failed\|error" $O/tests.log || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+tail -1 $O/smoke.log
+timeout -k 10 300 python bench.py > $O/default.json 2> $O/default.err || exit 1
+cat $O/default.json
+for r in 1 2; do
+  for w in cfg2 cfg4 cfg5; do
+    for m in "" "--per-step"; do
+      timeout -k 10 200 python bench.py --workload $w --no-cpu-baseline $m > $O/ab_${w}_${r}${m}.json 2>> $O/ab.err || exit 1
+      python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], sys.argv[3] or 'step_many', round(d['value']/1e6,1), 'M', round(d['ms_per_step']*1e3,2), 'us/step, kernel', round(d['roofline']['avg_kernel_us'],2))" $O/ab_${w}_${r}${m}.json $w "$m" | tee -a $O/ab_summary.txt
+    done
+  done
+done
