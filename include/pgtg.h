@@ -196,7 +196,7 @@ int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t rou
  * between launches (agent records, seeds, tile plans, all RNG streams with their buffered halves,
  * visited bitsets, both car banks, traffic records, spawner lists, map queue, counters) as one host
  * blob.  pgtg_state_size gives the blob size; pgtg_load_state accepts only a blob dumped from a handle
- * of the same config and batch size.  Outputs are not state: call pgtg_observe after a load to
+ * of the same config (checked by a hash of every configuration field) and batch size.  Outputs are not state: call pgtg_observe after a load to
  * re-emit the observations.  Both synchronise.  (No reference equivalent: PGTGEnv deep-copies
  * itself in light_step, environment.py:1283-1299.) */
 int pgtg_state_size(pgtg_handle* h, uint64_t* bytes);
@@ -211,6 +211,9 @@ int pgtg_set_to_state(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_
 int pgtg_set_rules(pgtg_handle* h, const PgtgRule* rules, int32_t n_rules);
 /* Re-emit the observation of every env into the bound outputs (after set_agent/add_car). */
 int pgtg_observe(pgtg_handle* h);
+/* Per-env uint64 digest of the car list into out_dev[N] (device; parity tests: the car term of
+ * pgtg_amd/digest.py).  Traffic handles only.  Asynchronous on the handle's stream. */
+int pgtg_car_digest(pgtg_handle* h, uint64_t* out_dev);
 /* steps (env-steps executed) and episodes (resets) since create, summed over envs; synchronises. */
 int pgtg_get_counters(pgtg_handle* h, uint64_t* env_steps, uint64_t* episodes);
 /* Number of envs whose last step reported an error (PGTG_E_DONE / PGTG_E_MAP); synchronises. */

@@ -1427,7 +1427,8 @@ int64_t orc_bench(const orc_config* cfg, int n_envs, int steps, uint64_t seed_ba
  * env g = env_offset + i: seeded with g, actions from the splitmix hash of (act_seed, t, g) (the
  * GPU's k_random_actions).  digest[t * n_envs + i] = pgtg_amd/digest.py's formula over that step's
  * outputs: sum of W(j) over the observation's set bytes j, W(D + k) times the small outputs, and the
- * terminal observation's bytes at W(D + 16 + j) when the env finished (all arithmetic mod 2^64). */
+ * terminal observation's bytes at W(D + 16 + j) when the env finished, and with traffic the car list
+ * after the step (dg_cars; all arithmetic mod 2^64). */
 static uint64_t dg_w(uint64_t j) {
   uint64_t z = j + 1 + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1449,6 +1450,20 @@ static uint64_t dg_small(const orc_out* o, int D, int nsd, int cost) {
   d += rb * dg_w(D + 4) + (uint64_t)(o->terminated != 0) * dg_w(D + 5) + (uint64_t)(o->truncated != 0) * dg_w(D + 6);
   if (nsd) d += (uint64_t)(int64_t)o->next_subgoal_direction * dg_w(D + 7);
   if (cost) d += cb * dg_w(D + 8);
+  return d;
+}
+/* car-list term of the digest (traffic handles): W(CB) x n_cars + per car j in list order
+ * W(CB + 1 + 2j) x (packed + 1) + W(CB + 2 + 2j) x patience, packed = id | x<<32 | y<<40 | route<<48 |
+ * profile<<53 | delay<<56 (pgtg_amd/digest.py car_term, the device's k_car_digest) */
+#define DG_CAR_BASE (1ull << 40)
+static uint64_t dg_cars(const orc_env* e) {
+  uint64_t d = (uint64_t)e->ncars * dg_w(DG_CAR_BASE);
+  for (int j = 0; j < e->ncars; j++) {
+    const car_t* c = &e->cars[j];
+    const uint64_t pk = (uint64_t)(uint32_t)c->id | (uint64_t)c->x << 32 | (uint64_t)c->y << 40 |
+                        (uint64_t)c->route << 48 | (uint64_t)c->profile << 53 | (uint64_t)c->delay << 56;
+    d += (pk + 1) * dg_w(DG_CAR_BASE + 1 + 2 * (uint64_t)j) + (uint64_t)(int64_t)c->patience * dg_w(DG_CAR_BASE + 2 + 2 * (uint64_t)j);
+  }
   return d;
 }
 int orc_rollout_digest(const orc_config* cfg, int64_t n_envs, uint64_t env_offset, int steps, uint64_t act_seed,
@@ -1494,6 +1509,7 @@ int orc_rollout_digest(const orc_config* cfg, int64_t n_envs, uint64_t env_offse
         step_out.next_subgoal_direction = out.next_subgoal_direction;
       }
       d += dg_obs(obs, D, 0) + dg_small(&step_out, D, cfg->next_subgoal, cfg->separate_reward_cost);
+      if (cfg->traffic_density > 0) d += dg_cars(e);
       digest[(size_t)t * (size_t)n_envs + (size_t)i] = d;
     }
     orc_destroy(e);

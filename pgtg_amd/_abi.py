@@ -32,7 +32,7 @@ EXPORTED = [
     "pgtg_get_map_plan", "pgtg_get_squares", "pgtg_set_rules", "pgtg_set_agent", "pgtg_add_car", "pgtg_observe", "pgtg_get_counters",
     "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_launch_info", "pgtg_occupancy", "pgtg_step_kernel", "pgtg_last_error", "pgtg_enable_timing",
     "pgtg_timing_read", "pgtg_measure_hbm", "pgtg_state_size", "pgtg_dump_state", "pgtg_load_state",
-    "pgtg_set_to_state",
+    "pgtg_set_to_state", "pgtg_car_digest",
 ]
 
 
@@ -127,6 +127,7 @@ def lib():
         "pgtg_add_car": ([vp, u64, i32, i32, i32, i32, i32], C.c_int),
         "pgtg_observe": ([vp], C.c_int),
         "pgtg_get_counters": ([vp, C.POINTER(u64), C.POINTER(u64)], C.c_int),
+        "pgtg_car_digest": ([vp, vp], C.c_int),
         "pgtg_error_count": ([vp, C.POINTER(u64), C.POINTER(i32)], C.c_int),
         "pgtg_window": ([vp], C.c_int),
         "pgtg_num_envs": ([vp], u64),

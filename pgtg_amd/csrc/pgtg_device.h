@@ -164,6 +164,7 @@ struct DevState {
   uint8_t* qstate;        // [n] or null
   uint8_t* err;           // [n] last error code (negated PGTG_E_*)
   unsigned long long* counters;  // [2]: env steps, episodes
+  unsigned long long* wg_ticks;  // [1]: wall-clock ticks of workgroup 0 in the last launch (start offsets)
   const int8_t* nsd_tab;
   const int8_t* cmp_tab;
 };
@@ -179,11 +180,6 @@ struct Pcg {
 };
 
 __device__ __forceinline__ void pcg_step(Pcg& g) {
-#ifdef PGTG_ABL_CHEAP_RNG  // diagnostic timing build only: NOT numpy's stream
-  g.slo = g.slo * 0x9E3779B97F4A7C15ull + g.ilo;
-  g.shi ^= g.slo;
-  return;
-#endif
   const uint64_t MH = 0x2360ED051FC65DA4ull, ML = 0x4385DF649FCCF645ull;
   uint64_t lo = g.slo * ML;
   uint64_t hi = __umul64hi(g.slo, ML) + g.slo * MH + g.shi * ML;

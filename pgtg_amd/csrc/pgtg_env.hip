@@ -44,11 +44,6 @@ __shared__ __attribute__((aligned(16))) Tables sT;  // per-workgroup LDS copy of
 // Copy the first `bytes` of the tables into sT: all of a thread's 16-byte loads are issued before
 // the first LDS store (one memory latency instead of one per word).
 __device__ __forceinline__ void stage_tables(const Tables* __restrict__ gtab, int bytes) {
-#ifdef PGTG_OLD_STAGE  // A/B build only
-  for (int k = threadIdx.x; k < bytes / 4; k += kBlock)
-    reinterpret_cast<uint32_t*>(&sT)[k] = reinterpret_cast<const uint32_t*>(gtab)[k];
-  return;
-#endif
   const int n4 = bytes >> 4, tid = (int)threadIdx.x;
   const uint4* src = reinterpret_cast<const uint4*>(gtab);
   uint4* dst = reinterpret_cast<uint4*>(&sT);
@@ -66,13 +61,9 @@ __device__ __forceinline__ void stage_tables(const Tables* __restrict__ gtab, in
 // Workgroup barrier for LDS data only: unlike __syncthreads() it does not wait for the waves'
 // outstanding global stores (outputs, state) to complete.
 __device__ __forceinline__ void lds_barrier() {
-#ifdef PGTG_FULL_FENCE  // A/B build only
-  __syncthreads();
-#else
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#endif
 }
 
 // One env's tile plan (plan_stride u16 words in HBM, a multiple of 8, <= 64) into its LDS row of
@@ -80,16 +71,6 @@ __device__ __forceinline__ void lds_barrier() {
 __device__ __forceinline__ void stage_plan(const uint16_t* __restrict__ plan, int plan_stride, uint32_t* dst, int pdw) {
   const uint4* src = reinterpret_cast<const uint4*>(plan);
   const int nq = plan_stride / 8;
-#ifdef PGTG_OLD_STAGE  // A/B build only
-  for (int k = 0; k < nq; k++) {
-    const uint4 w4 = src[k];
-    const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (k * 4 + j < pdw) dst[k * 4 + j] = wv[j];
-  }
-  return;
-#endif
   uint4 q[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) q[k] = src[k < nq ? k : 0];  // unconditional: registers, not scratch
@@ -404,9 +385,6 @@ __device__ __forceinline__ M expand_sym(M R, M hN, M hE, M hS, M hW, int w) {
 // component is exhausted first, in which case s-g broke iff exactly one of s, g lies in it.
 template <typename M>
 __device__ __forceinline__ bool still_connected(M hN, M hE, M hS, M hW, int w, int a, int b, int s, int g) {
-#ifdef PGTG_ABL_NOBFS  // diagnostic timing build only
-  return ((hN ^ hS) >> a) & 1;
-#endif
   // Two expansions per side between checks: the sets only grow, so meeting and exhaustion are
   // still detected (at most one expansion late) with half the loop control of a step-wise loop.
   // One exit condition keeps the loop's mask bookkeeping short.
@@ -445,11 +423,7 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, 
   // the end of the iteration, before the following draw.
   auto draw_edge = [&](int n) {
     const int k = (int)pcg_draw(r, true, (uint32_t)n);  // n >= 2: always draws
-#ifdef PGTG_ABL_NOSELECT  // diagnostic timing build only
-    const int e = k;
-#else
     const int e = L.select(k);
-#endif
     L.clear(e);
     return e;
   };
@@ -1801,11 +1775,11 @@ struct Lds {
   int queue;           // step launches use k_envq (maps generated one episode ahead by helper waves)
   int gen_off;         // k_envq: word offset of the helper lanes' plan scratch (kQueueLanes x plan_stride_dw)
   int lm_words;        // terminal-observation line mask words (0: test the selection bytes)
-  int diag;            // diagnostic experiments (PGTG_DIAG; 0 in normal runs)
-  int stagger_ticks;   // first-round start offsets: workgroup b < stagger_wgs waits b/stagger_wgs of this (100 MHz ticks)
+  int stagger;         // first-round start offsets (stagger_start) on
   int stagger_wgs;     // workgroups resident in the first round (blocks per CU x CUs)
 };
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
+constexpr uint64_t kStaggerMaxTicks = 20000;  // 200 us of 100 MHz wall clock: a bound, never reached
 constexpr int kQueueDepth = 3;   // queued maps per env (a ring)
 
 __host__ __device__ inline int odd_up(int x) { return x | 1; }
@@ -1832,14 +1806,12 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   // map queue: random maps without traffic or braking rules (k_envq), a whole-workgroup observation
   // image and at least one wave without env slots
   l.queue = !c.need_car && c.n_rules == 0 && !c.fixed_map && envs <= kBlock - 64 && l.sub_envs >= envs;
-  l.diag = 0;
-  l.stagger_ticks = 0;
+  l.stagger = 0;
   l.stagger_wgs = 0;
 #ifdef PGTG_TUNING  // A/B and diagnostic builds only: the product library reads no environment
   if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);
   if (const char* e = getenv("PGTG_COMPACT")) l.compact = atoi(e);
   if (const char* e = getenv("PGTG_QUEUE")) l.queue = l.queue && atoi(e);
-  if (const char* e = getenv("PGTG_DIAG")) l.diag = atoi(e);
 #endif
   lds_tail(l, c);
   return l;
@@ -1907,11 +1879,21 @@ __device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, con
 // and compute in the same windows.  Offsetting the first round's starts along a ramp keeps the
 // offsets for every later round (a finishing workgroup's slot takes the next one at once), so the
 // write phases of some workgroups overlap the compute phases of others.
-__device__ __forceinline__ void stagger_start(const Lds& L) {
-  if (L.stagger_ticks <= 0 || blockIdx.x >= (unsigned)L.stagger_wgs) return;
-  const uint64_t wait = (uint64_t)L.stagger_ticks * blockIdx.x / (unsigned)L.stagger_wgs;
+// The ramp is half of the workgroup duration the previous launch measured (workgroup 0's, in
+// wall-clock ticks, S.wg_ticks), so it follows the phase length of whatever the kernel does on this
+// device instead of a tuned constant; the first launch of a handle runs without offsets.
+__device__ __forceinline__ uint64_t stagger_start(const Lds& L, const DevState& S) {
+  if (!L.stagger) return 0;
   const uint64_t t0 = wall_clock64();
+  if (blockIdx.x == 0 || blockIdx.x >= (unsigned)L.stagger_wgs) return t0;
+  const uint64_t span = min(S.wg_ticks[0] / 2ull, (unsigned long long)kStaggerMaxTicks);
+  const uint64_t wait = span * blockIdx.x / (unsigned)L.stagger_wgs;
   while (wall_clock64() - t0 < wait) __builtin_amdgcn_s_sleep(16);
+  return t0;
+}
+// workgroup 0 records its duration for the next launch's ramp (timing only: not part of any result)
+__device__ __forceinline__ void stagger_record(const Lds& L, const DevState& S, uint64_t t0) {
+  if (L.stagger && blockIdx.x == 0 && threadIdx.x == 0) S.wg_ticks[0] = wall_clock64() - t0;
 }
 
 template <bool TR>
@@ -1922,7 +1904,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   extern __shared__ uint32_t lds[];
   const DevCfg& c = *cfg;
   const int tid = threadIdx.x;
-  if (!TR) stagger_start(L);
+  const uint64_t t_start = TR ? 0 : stagger_start(L, S);
   STAMP(0);
   // the traffic-reset list of the next launch starts empty (its previous consumer has finished)
   if ((TR && c.need_car) && mode != MODE_OBSERVE && blockIdx.x == 0 && tid == 0) S.tr_count[tr_slot ^ 1u] = 0u;
@@ -2172,6 +2154,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
                  slot);
   }
   if (mode == MODE_STEP && tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
+  if (!TR) stagger_record(L, S, t_start);
   STAMP(6);
 }
 
@@ -2225,18 +2208,10 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
 // LDS-only fences: the waves exchange LDS data only, so their global stores stay in flight across
 // the barrier (a plain workgroup fence waits for every outstanding global access first).
 __device__ __forceinline__ void sub_barrier(uint32_t* ctr, uint32_t target) {
-#ifdef PGTG_FULL_FENCE  // A/B build only
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-#else
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-#endif
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
-#ifdef PGTG_FULL_FENCE
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#endif
 }
 
 // Step launch with the map queue (no traffic; workgroups of <= 192 envs).  Wave `env_waves` (the
@@ -2289,7 +2264,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   extern __shared__ uint32_t lds[];
   const DevCfg& c = *cfg;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  stagger_start(L);
+  const uint64_t t_start = stagger_start(L, S);
   STAMP(0);
   stage_tables(gtab, (int)(c.generic_channels ? sizeof(Tables) : offsetof(Tables, lanes)));
   const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
@@ -2372,9 +2347,6 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
         l++;
       }
       if (l < kQueueDepth) refill(k, l);
-#ifdef PGTG_TUNING
-      if (L.diag == 8 && l < kQueueDepth) refill(k, l);  // diagnostic: the same (deterministic) refill twice
-#endif
     }
     STAMP(7);
     return;
@@ -2497,6 +2469,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   if (out.obs)
     write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr, rank, nthr);
   if (tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
+  stagger_record(L, S, t_start);
   STAMP(6);
 }
 
@@ -2647,18 +2620,53 @@ __global__ void k_random_actions(uint8_t* a, uint64_t n, uint64_t seed, uint64_t
 }
 
 // Stream copy: the measured HBM denominator of the roofline (pgtg_measure_hbm).  16 B per lane,
-// U independent loads in flight per lane, grid-stride.
-template <int U>
-__global__ void __launch_bounds__(256) k_hbm_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n16) {
+// U independent loads in flight per lane, grid-stride (a grid covering the buffer copies it in one
+// pass); NT: nontemporal loads and stores (streamed data bypasses the caches' retention).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) k_hbm_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n16) {
   const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
   for (uint64_t b = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; b < n16; b += stride) {
-    uint4 r[U];
+    u32x4 r[U];
 #pragma unroll
-    for (int j = 0; j < U; j++) r[j] = src[b + j * 256 < n16 ? b + j * 256 : b];
+    for (int j = 0; j < U; j++) {
+      const uint64_t k = b + j * 256 < n16 ? b + j * 256 : b;
+      r[j] = NT ? __builtin_nontemporal_load(src + k) : src[k];
+    }
 #pragma unroll
     for (int j = 0; j < U; j++)
-      if (b + j * 256 < n16) dst[b + j * 256] = r[j];
+      if (b + j * 256 < n16) {
+        if (NT) __builtin_nontemporal_store(r[j], dst + b + j * 256);
+        else dst[b + j * 256] = r[j];
+      }
   }
+}
+
+// Per-env digest term of the car list (pgtg_amd/digest.py car_term, oracle dg_cars): the cars in
+// list order (slot order, empty slots skipped), coalesced slot rows.  Test/parity infrastructure.
+__device__ __forceinline__ uint64_t dg_w(uint64_t j) {
+  uint64_t z = j + 1 + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ void __launch_bounds__(256) k_car_digest(DevState S, uint64_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S.n) return;
+  constexpr uint64_t CB = 1ull << 40;
+  const uint4 t = S.traf[i];
+  const CarSlots cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
+  uint64_t d = (uint64_t)(t.x & 0xffffu) * dg_w(CB), j = 0;
+  for (int k = 0; k < (int)t.z; k++) {
+    const uint32_t w0 = cs.w0[cs.at(k)];
+    if (w0 & kCarEmpty) continue;
+    const uint64_t pk = (uint64_t)cs.id[cs.at(k)] | (uint64_t)(w0 & 255u) << 32 | (uint64_t)((w0 >> 8) & 255u) << 40 |
+                        (uint64_t)((w0 >> 16) & 31u) << 48 | (uint64_t)((w0 >> 21) & 7u) << 53 |
+                        (uint64_t)((w0 >> 24) & 3u) << 56;
+    d += (pk + 1) * dg_w(CB + 1 + 2 * j) + (uint64_t)cs.w1[cs.at(k)] * dg_w(CB + 2 + 2 * j);
+    j++;
+  }
+  out[i] = d;
 }
 
 __global__ void k_fill_seeds(uint64_t* seed, uint64_t n, uint64_t base, uint64_t offset) {
@@ -3118,9 +3126,9 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
     // only launches of several rounds: one round has no later workgroups to keep the offsets
     // (1 048 576 5x5 envs, 8 rounds: k_envq 476 -> 460 us; one round: slower)
     const uint64_t blocks = (h->n + h->L.envs - 1) / h->L.envs;
-    h->L.stagger_ticks = blocks >= (uint64_t)3 * h->L.stagger_wgs ? 2500 : 0;
+    h->L.stagger = blocks >= (uint64_t)3 * h->L.stagger_wgs ? 1 : 0;
 #ifdef PGTG_TUNING
-    if (const char* e = getenv("PGTG_STAGGER")) h->L.stagger_ticks = atoi(e);
+    if (const char* e = getenv("PGTG_STAGGER")) h->L.stagger = atoi(e);
 #endif
   }
   return PGTG_OK;
@@ -3166,6 +3174,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
   ALLOC(S.plan, n * (uint64_t)c.plan_stride);
   ALLOC(S.err, n);
   ALLOC(S.counters, 2);
+  ALLOC(S.wg_ticks, 1);
   DevStream* streams[4] = {&S.car, &S.ice, &S.broken, &S.sand};
   int needs[4] = {c.need_car, c.need_ice, c.need_broken, c.need_sand};
   for (int k = 0; k < 4; k++)
@@ -3621,12 +3630,19 @@ struct PgtgStateHeader {
   uint64_t n;
   uint32_t n_sections, nt, car_cap, plan_stride;
   uint32_t max_spawners, vis_words, qrec_dw, car_slots;
+  uint64_t cfg_hash;  // FNV-1a of the handle's DevCfg: every semantic field (probabilities, rewards, map, rules)
 };
 struct PgtgSectionEntry {
   uint32_t id, pad;
   uint64_t bytes;
 };
-constexpr uint32_t kStateVersion = 2;
+constexpr uint32_t kStateVersion = 3;
+uint64_t cfg_hash(const DevCfg& c) {  // DevCfg is zero-initialised (derive_cfg), so padding hashes as 0
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(&c);
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (size_t k = 0; k < sizeof c; k++) h = (h ^ p[k]) * 0x100000001b3ull;
+  return h;
+}
 }  // namespace
 
 static std::vector<StateSection> state_sections(pgtg_handle* h) {
@@ -3692,6 +3708,7 @@ int pgtg_dump_state(pgtg_handle* h, void* buf, uint64_t bytes) {
   hd.vis_words = (uint32_t)h->hcfg.vis_words;
   hd.qrec_dw = (uint32_t)h->hcfg.qrec_dw;
   hd.car_slots = (uint32_t)h->hcfg.car_slots;
+  hd.cfg_hash = cfg_hash(h->hcfg);
   memcpy(p, &hd, sizeof hd);
   uint64_t off = sizeof hd;
   for (const auto& s : v) {
@@ -3722,6 +3739,8 @@ int pgtg_load_state(pgtg_handle* h, const void* buf, uint64_t bytes) {
       hd.qrec_dw != (uint32_t)h->hcfg.qrec_dw || hd.car_slots != (uint32_t)h->hcfg.car_slots ||
       bytes < state_blob_bytes(v))
     return fail(h, PGTG_E_INVALID, "pgtg_load_state: the state was dumped from a handle of another shape");
+  if (hd.cfg_hash != cfg_hash(h->hcfg))
+    return fail(h, PGTG_E_INVALID, "pgtg_load_state: the state was dumped from a handle of another configuration");
   uint64_t off = sizeof hd;
   for (const auto& s : v) {
     PgtgSectionEntry e;
@@ -3774,6 +3793,15 @@ int pgtg_set_to_state(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_
     for (int k = 0; k < n_cars; k++) v.push_back(PgtgCar{cars[k].id, cars[k].x, cars[k].y, cars[k].route, cars[k].profile, 0, 0});
     if (int rc = host_write_cars(h, env, t, v, n_cars > 0 ? (uint32_t)cars[n_cars - 1].id + 1u : t.y)) return rc;
   }
+  return PGTG_OK;
+}
+
+int pgtg_car_digest(pgtg_handle* h, uint64_t* out_dev) {
+  if (!h || !out_dev) return PGTG_E_INVALID;
+  if (!h->hcfg.need_car) return fail(h, PGTG_E_UNSUPPORTED, "pgtg_car_digest: the handle has no traffic");
+  HIPCHK(h, hipSetDevice(h->device));
+  hipLaunchKernelGGL(k_car_digest, dim3((unsigned)((h->n + 255) / 256)), dim3(256), 0, h->stream, h->S, out_dev);
+  HIPCHK(h, hipGetLastError());
   return PGTG_OK;
 }
 
@@ -3851,28 +3879,34 @@ int pgtg_measure_hbm(int32_t device, uint64_t bytes, int32_t reps, double* copy_
       hipMemset(a, 1, n16 * 16) == hipSuccess && hipMemset(b, 2, n16 * 16) == hipSuccess &&
       hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
     rc = PGTG_OK;
-    for (int u = 0; u < 2 && rc == PGTG_OK; u++)
-      for (int wpc = 4; wpc <= 16 && rc == PGTG_OK; wpc *= 2) {
-        const int U = u ? 8 : 4;
-        const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)ncu * wpc, (n16 + 256 * U - 1) / (256 * U));
-        auto pass = [&](int r) {
-          const uint4* src = (const uint4*)((r & 1) ? b : a);
-          uint4* dst = (uint4*)((r & 1) ? a : b);
-          if (U == 8) hipLaunchKernelGGL(k_hbm_copy<8>, dim3(grid), dim3(256), 0, 0, src, dst, n16);
-          else hipLaunchKernelGGL(k_hbm_copy<4>, dim3(grid), dim3(256), 0, 0, src, dst, n16);
-        };
-        pass(0);  // untimed: page-in, clocks
-        (void)hipEventRecord(e0, 0);
-        for (int r = 0; r < reps; r++) pass(r);
-        (void)hipEventRecord(e1, 0);
-        float ms = 0.f;
-        if (hipGetLastError() != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
-            hipEventElapsedTime(&ms, e0, e1) != hipSuccess || !(ms > 0.f)) {
-          rc = PGTG_E_DEVICE;
-          break;
-        }
-        best = std::max(best, 2.0 * (double)(n16 * 16) * reps / (ms * 1e-3) / 1e9);  // read + write bytes
+    // shapes: loads in flight per lane (1, 4), plain or nontemporal, workgroups per CU (4, 8, 16)
+    // or one pass over the buffer (wpc 0: a workgroup per 256 x U chunks)
+    for (int shape = 0; shape < 16 && rc == PGTG_OK; shape++) {
+      const int U = (shape & 1) ? 4 : 1;
+      const bool nt = (shape >> 1) & 1;
+      const int wpc = (shape >> 2) == 0 ? 0 : (4 << ((shape >> 2) - 1));
+      const uint64_t full = (n16 + 256 * U - 1) / (256 * U);
+      const unsigned grid = (unsigned)(wpc ? std::min<uint64_t>((uint64_t)ncu * wpc, full) : std::min<uint64_t>(full, 1u << 30));
+      auto pass = [&](int r) {
+        const u32x4* src = (const u32x4*)((r & 1) ? b : a);
+        u32x4* dst = (u32x4*)((r & 1) ? a : b);
+        if (U == 4 && nt) hipLaunchKernelGGL((k_hbm_copy<4, true>), dim3(grid), dim3(256), 0, 0, src, dst, n16);
+        else if (U == 4) hipLaunchKernelGGL((k_hbm_copy<4, false>), dim3(grid), dim3(256), 0, 0, src, dst, n16);
+        else if (nt) hipLaunchKernelGGL((k_hbm_copy<1, true>), dim3(grid), dim3(256), 0, 0, src, dst, n16);
+        else hipLaunchKernelGGL((k_hbm_copy<1, false>), dim3(grid), dim3(256), 0, 0, src, dst, n16);
+      };
+      pass(0);  // untimed: page-in, clocks
+      (void)hipEventRecord(e0, 0);
+      for (int r = 0; r < reps; r++) pass(r);
+      (void)hipEventRecord(e1, 0);
+      float ms = 0.f;
+      if (hipGetLastError() != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+          hipEventElapsedTime(&ms, e0, e1) != hipSuccess || !(ms > 0.f)) {
+        rc = PGTG_E_DEVICE;
+        break;
       }
+      best = std::max(best, 2.0 * (double)(n16 * 16) * reps / (ms * 1e-3) / 1e9);  // read + write bytes
+    }
   }
   if (rc == PGTG_OK) *copy_gbs = best;
   if (e0) (void)hipEventDestroy(e0);

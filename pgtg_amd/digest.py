@@ -2,8 +2,10 @@
 
 A digest condenses one env's step outputs into a uint64 (arithmetic mod 2^64, held in int64
 tensors): the sum of W(j) over the observation bytes j that are set, W(D + k) times the small
-outputs (position, velocity, reward bits, terminated, truncated, next-subgoal direction, cost bits)
-and, for an env that finished this step, its terminal observation's set bytes at W(D + 16 + j).
+outputs (position, velocity, reward bits, terminated, truncated, next-subgoal direction, cost bits),
+for an env that finished this step its terminal observation's set bytes at W(D + 16 + j), and for
+traffic handles the car list after the step (`car_term`: every car's id, square, route, profile,
+delay and patience in list order, computed on the device by pgtg_car_digest).
 W is the splitmix64 finaliser of j + 1.  The CPU restatement computes the same formula
 (oracle/pgtg_oracle.c `orc_rollout_digest`), so a whole batch can be compared env by env at every
 step without copying observations to the host; sharded runs compare their slices with a
@@ -23,6 +25,20 @@ def _w(j: int) -> int:
 
 def _signed(u: int) -> int:
     return u - (1 << 64) if u >= 1 << 63 else u
+
+
+CAR_BASE = 1 << 40
+
+
+def car_term(cars) -> int:
+    """Car-list term of an env's digest (uint64 as a Python int): cars = rows (id, x, y, route,
+    profile, patience, delay) in list order (PGTGVecEnv.cars / OracleEnv.cars).  The same formula as
+    the device kernel k_car_digest and oracle/pgtg_oracle.c dg_cars."""
+    d = (len(cars) * _w(CAR_BASE)) & _M64
+    for j, (cid, x, y, route, prof, pat, delay) in enumerate(cars):
+        pk = (int(cid) & 0xFFFFFFFF) | int(x) << 32 | int(y) << 40 | int(route) << 48 | int(prof) << 53 | int(delay) << 56
+        d = (d + (pk + 1) * _w(CAR_BASE + 1 + 2 * j) + (int(pat) & _M64) * _w(CAR_BASE + 2 + 2 * j)) & _M64
+    return d
 
 
 class Digest:
@@ -65,4 +81,6 @@ class Digest:
         if e.final_map is not None:
             done = (e.terminated | e.truncated).to(torch.int64)
             d += self._obs_sum(e.final_map, self.w_fin) * done
+        if getattr(e, "has_cars", False):
+            d += e.car_digest()
         return d

@@ -34,11 +34,14 @@ def from_env(n_local: int) -> Shard:
     return Shard(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), int(n_local))
 
 
-def reduce_counters(env_steps: int, episodes: int, elapsed_s: float, device=None) -> tuple[int, int, float]:
-    """(sum env-steps, sum episodes, max elapsed) over ranks; identity without a process group."""
+def reduce_counters(env_steps: int, episodes: int, elapsed_s: float, device=None,
+                    force: bool = False) -> tuple[int, int, float]:
+    """(sum env-steps, sum episodes, max elapsed) over ranks; identity without a process group.
+    `force`: run the collectives even in a one-rank group (exercises RCCL init and the device
+    all-reduce on a one-GPU box)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()) or (dist.get_world_size() == 1 and not force):
         return int(env_steps), int(episodes), float(elapsed_s)
     cnt = torch.tensor([env_steps, episodes], dtype=torch.int64, device=device)
     tim = torch.tensor([elapsed_s], dtype=torch.float64, device=device)

@@ -85,6 +85,7 @@ class PGTGVecEnv:
         o.final_velocity, o.final_next_subgoal = ptr(self.final_velocity), ptr(self.final_nsd)
         self._outs = o
         _check(self._lib.pgtg_set_outputs(h, C.byref(o)), h)
+        self.has_cars = self.spec.traffic_density > 0 or min_car_capacity > 0  # the handle keeps car lists
         self._seeded = False
 
     # -- plumbing ------------------------------------------------------------------------------
@@ -162,8 +163,12 @@ class PGTGVecEnv:
             actions = torch.as_tensor(host.astype(np.uint8))
         elif actions.numel() != self.num_envs:
             raise ValueError(f"expected {self.num_envs} actions, got {actions.numel()}")
-        elif bool(((actions < 0) | (actions > 8)).any()):  # one device sync; step_actions() skips it
-            raise KeyError("action outside Discrete(9)")
+        elif actions.dtype != torch.uint8 or actions.device.type != "cuda":
+            # other dtypes / host tensors: range-checked here (a uint8 device tensor is not: the check
+            # would be a device sync per step; the kernel records PGTG_E_INVALID per env instead, and
+            # non-autoreset handles raise it below; autoreset callers read error_count())
+            if bool(((actions < 0) | (actions > 8)).any()):
+                raise KeyError("action outside Discrete(9)")
         a = actions
         if a.device != self.device or a.dtype != torch.uint8:
             a = a.to(device=self.device, dtype=torch.uint8)
@@ -208,8 +213,9 @@ class PGTGVecEnv:
     def step_many(self, actions):
         """len(actions) ticks from a resident [T, N] uint8 device tensor in one host call
         (include/pgtg.h pgtg_step_many); the outputs hold the last tick's."""
-        if actions.dim() != 2 or actions.shape[1] != self.num_envs or actions.dtype.itemsize != 1:
-            raise ValueError(f"expected a [T, {self.num_envs}] uint8 tensor, got {tuple(actions.shape)}")
+        import torch
+        if actions.dim() != 2 or actions.shape[1] != self.num_envs or actions.dtype != torch.uint8:
+            raise ValueError(f"expected a [T, {self.num_envs}] uint8 tensor, got {tuple(actions.shape)} {actions.dtype}")
         if actions.device != self.device or actions.stride(1) != 1:
             raise ValueError("actions must be a row-contiguous tensor on the env's device")
         self._bind_stream()
@@ -221,6 +227,14 @@ class PGTGVecEnv:
         self._bind_stream()
         _check(self._lib.pgtg_observe(self._h), self._h)
         return self.observation()
+
+    def error_count(self) -> tuple[int, int]:
+        """(envs whose last step failed, first error code); e.g. PGTG_E_INVALID for an action > 8
+        passed in a uint8 device tensor, which step() does not range-check."""
+        n = C.c_uint64()
+        code = C.c_int32()
+        _check(self._lib.pgtg_error_count(self._h, C.byref(n), C.byref(code)), self._h)
+        return n.value, code.value
 
     def _raise_errors(self):
         n = C.c_uint64()
@@ -345,6 +359,14 @@ class PGTGVecEnv:
     def step_kernel(self) -> str:
         """Name of the kernel(s) a step launches (measurement labels)."""
         return self._lib.pgtg_step_kernel(self._h).decode()
+
+    def car_digest(self):
+        """Per-env digest of the car lists (int64 [N] device tensor; pgtg_amd/digest.py car_term)."""
+        import torch
+        out = torch.empty(self.num_envs, dtype=torch.int64, device=self.device)
+        self._bind_stream()
+        _check(self._lib.pgtg_car_digest(self._h, C.c_void_p(out.data_ptr())), self._h)
+        return out
 
     def counters(self) -> tuple[int, int]:
         a, b = C.c_uint64(), C.c_uint64()

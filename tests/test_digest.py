@@ -11,7 +11,7 @@ import helpers  # noqa: F401
 from oracle import oracle
 from oracle.oracle import OracleEnv
 from pgtg_amd import config as cfg
-from pgtg_amd.digest import Digest
+from pgtg_amd.digest import Digest, car_term
 
 M64 = (1 << 64) - 1
 
@@ -30,6 +30,7 @@ def action(seed: int, t: int, g: int) -> int:
     dict(random_map_width=4, random_map_height=4, use_next_subgoal_direction=True, separate_reward_cost=True,
          random_map_obstacle_probability=0.5, standing_still_penalty=0.5),
     dict(random_map_width=3, random_map_height=3, traffic_density=0.3, use_sliding_observation_window=True),
+    dict(random_map_width=4, random_map_height=3, traffic_density=0.5),
 ])
 def test_digest_formula_matches_oracle(kw):
     spec = cfg.make_spec(**kw)
@@ -59,5 +60,8 @@ def test_digest_formula_matches_oracle(kw):
         fake.truncated = torch.tensor([r["truncated"] for r in rs])
         fake.nsd = torch.tensor([r["nsd"] for r in rs], dtype=torch.int32) if spec.next_subgoal else None
         fake.cost = torch.tensor([r["cost"] for r in rs], dtype=torch.float64) if spec.separate_reward_cost else None
+        fake.has_cars = spec.traffic_density > 0
+        terms = [car_term(e.cars()) for e in envs]
+        fake.car_digest = lambda: torch.tensor(np.array(terms, dtype=np.uint64).view(np.int64))
         got = dg.step_digest().numpy().view(np.uint64)
         assert np.array_equal(got, ref[t]), f"t{t}: {np.nonzero(got != ref[t])[0][:5]}"

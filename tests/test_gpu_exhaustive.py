@@ -7,7 +7,8 @@ formulas to each other), so whole batches are compared without copying them to t
   configs[1]  4 096 envs x 100 steps, 3x3 maps                    (SURVEY.md 8(d) cfg 2)
   configs[3]  262 144 envs x 20 steps, 3x3 maps, in-kernel resets
   configs[4]  1 048 576 envs x 10 steps, 5x5 maps (the bench line; grid indexing past 2^20 envs)
-  configs[2]  65 536 envs x 3 steps, 5x5 maps, traffic 0.5 (every env's initial traffic), plus
+  configs[2]  65 536 envs x 40 steps, 5x5 maps, traffic 0.5, with every env's car list in the
+              digest (id, square, route, profile, patience, delay of every car after every step), plus
               256 envs x 120 steps of cautious driving with the car lists compared (patience,
               crowded squares, spawner lists beyond the staged first 24)
   feature variants at batch sizes of every launch shape, incl. forced workgroup/sub-batch shapes.
@@ -66,7 +67,7 @@ CASES = {
     "cfg2_all_4096x100": (4096, 100, dict(random_map_width=3, random_map_height=3), None),
     "cfg4_all_262144x20": (262144, 20, dict(random_map_width=3, random_map_height=3), None),
     "cfg5_all_1048576x10": (1048576, 10, dict(random_map_width=5, random_map_height=5), None),
-    "cfg3_all_65536x3": (65536, 3, dict(random_map_width=5, random_map_height=5, traffic_density=0.5), None),
+    "cfg3_all_65536x40": (65536, 40, dict(random_map_width=5, random_map_height=5, traffic_density=0.5), None),
     # feature variants over the launch shapes (16/32/64/128/256 envs per workgroup, sub-batched images)
     "obstacles_40000": (40000, 15, dict(random_map_width=4, random_map_height=4, random_map_obstacle_probability=1.0,
                                         random_map_ice_probability_weight=1, random_map_broken_road_probability_weight=1,

@@ -77,19 +77,22 @@ def test_load_state_rejects_other_shapes():
     a = PGTGVecEnv(64, spec=_spec(CONFIGS["s3_queue"]), device=0)
     b = PGTGVecEnv(65, spec=_spec(CONFIGS["s3_queue"]), device=0)
     c = PGTGVecEnv(64, spec=_spec(CONFIGS["traffic"]), device=0)
+    # same shape, other semantics: a different obstacle probability / crash penalty
+    d = PGTGVecEnv(64, spec=_spec(dict(CONFIGS["s3_queue"], crash_penalty=7)), device=0)
+    e = PGTGVecEnv(64, spec=_spec(dict(CONFIGS["s3_queue"], random_map_percentage_of_connections=0.7)), device=0)
+    same = PGTGVecEnv(64, spec=_spec(CONFIGS["s3_queue"]), device=0)
     try:
         a.reset(seed=1)
         blob = a.dump_state()
-        with pytest.raises(ValueError):
-            b.load_state(blob)
-        with pytest.raises(ValueError):
-            c.load_state(blob)
+        for other in (b, c, d, e):
+            with pytest.raises(ValueError):
+                other.load_state(blob)
         with pytest.raises(ValueError):
             a.load_state(blob[:100])
+        same.load_state(blob)  # a handle of the same config accepts it
     finally:
-        a.close()
-        b.close()
-        c.close()
+        for h in (a, b, c, d, e, same):
+            h.close()
 
 
 @pytest.mark.parametrize("fixture", ["smallest_simple_env", "simple_env", "obstacle_env"])
@@ -209,6 +212,21 @@ def test_save_map_round_trip(tmp_path, seed):
     fixed.close()
 
 
+def _sections(a, b):
+    """{section id: (bytes of a, bytes of b)} of two pgtg_dump_state blobs (layout: PgtgStateHeader,
+    n_sections x {id u32, pad u32, bytes u64}, each section at a 16-byte aligned offset)."""
+    hdr = 4 + 4 + 8 + 4 * 4 + 4 * 4 + 8
+    n_sec = int(np.frombuffer(a[16:20].tobytes(), np.uint32)[0])
+    ent = np.frombuffer(a[hdr:hdr + 16 * n_sec].tobytes(), dtype=[("id", "<u4"), ("pad", "<u4"), ("bytes", "<u8")])
+    off, out = hdr + 16 * n_sec, {}
+    for e in ent:
+        off = (off + 15) & ~15
+        out[int(e["id"])] = (a[off:off + int(e["bytes"])], b[off:off + int(e["bytes"])])
+        off += int(e["bytes"])
+    assert off == a.size, (off, a.size)
+    return out
+
+
 @pytest.mark.parametrize("name", ["s3_queue", "traffic"])
 def test_step_many_equals_step_loop(name):
     """pgtg_step_many (one host call for T ticks from a [T, N] buffer) == T pgtg_step calls: the
@@ -228,8 +246,12 @@ def test_step_many_equals_step_loop(name):
         da, db = Digest(a).step_digest().cpu().numpy(), Digest(b).step_digest().cpu().numpy()
         assert np.array_equal(da, db), f"{name}: digests differ at {np.argwhere(da != db)[:5]}"
         assert a.counters() == b.counters()
-        # the state blobs may differ in how far each handle's map-queue rings were filled ahead (a
-        # timing matter); what follows from the state must not: 8 more ticks on both
+        # identical work leaves identical state: every section of the blob (agent records, plans,
+        # RNG streams, car slots, spawner lists, map-queue rings and their counts) byte for byte
+        sa, sb = a.dump_state(), b.dump_state()
+        assert sa.size == sb.size
+        diff = [sec for sec, (x, y) in _sections(sa, sb).items() if not np.array_equal(x, y)]
+        assert not diff, f"{name}: state sections differ: {diff}"
         more = a.random_actions(8, 0x5EED, t0=k)
         ra, rb = _rollout(a, Digest(a), more, 0, 8), _rollout(b, Digest(b), more, 0, 8)
         assert np.array_equal(ra, rb), f"{name}: later ticks differ at {np.argwhere(ra != rb)[:5]}"

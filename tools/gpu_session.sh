@@ -1,0 +1,65 @@
+#!/bin/bash
+# One GPU call made of named steps, each under its own time limit; the first failing step ends the
+# call.  Output under gpurun_out/<tag>/.  Usage: bash tools/gpu_session.sh <tag> <step>...
+#   tests            pytest -m gpu (whole suite)
+#   tests:<expr>     pytest -m gpu -k <expr>
+#   smoke            __graft_entry__.smoke()
+#   bench            the default bench line (configs[4], with the CPU baseline)
+#   bench:<wl>       bench.py --workload <wl> --steps 200 --warmup 20
+#   rccl             bench.py under torch.distributed.run, one rank, nccl backend, --dist (RCCL init +
+#                    the device counter all-reduce), 131 072 envs
+#   shards           single-process lines at the per-rank shards of N = 2, 4, 8 (524 288 / 262 144 /
+#                    131 072 envs) beside the 1 048 576-env line
+#   profile:<wl,..>  tools/gpu_profile.sh (rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes)
+#   stamps:<wl,..>   per-phase cycle stamps (PGTG_STAMPS build, tools/stamps.py)
+#   ab:<wl>:<lib>    interleaved bench lines of the in-tree library and <lib> (tools/ab_multi.sh, 3 reps)
+set -o pipefail
+TAG=$1
+shift
+O=gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+for S in "$@"; do
+  echo "== $S $(date +%T)"
+  case $S in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/pytest.log 2>&1
+      rc=$?; tail -3 $O/pytest.log; [ $rc = 0 ] || exit 1 ;;
+    tests:*)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -k "${S#tests:}" > $O/pytest_k.log 2>&1
+      rc=$?; tail -5 $O/pytest_k.log; [ $rc = 0 ] || exit 1 ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+      tail -2 $O/smoke.log ;;
+    bench)
+      timeout -k 10 400 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
+      cat $O/bench_default.json ;;
+    bench:*)
+      W=${S#bench:}
+      timeout -k 10 300 python -u bench.py --workload $W --steps 200 --warmup 20 --no-cpu-baseline > $O/bench_$W.json 2> $O/bench_$W.err || { tail -20 $O/bench_$W.err; exit 1; }
+      python tools/bench_line.py $O/bench_$W.json ;;
+    rccl)
+      timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+        --master-port 29517 bench.py --dist --envs 131072 --steps 200 --warmup 20 --no-cpu-baseline \
+        > $O/rccl.json 2> $O/rccl.err || { tail -30 $O/rccl.err; exit 1; }
+      cat $O/rccl.json ;;
+    shards)
+      for N in 1048576 524288 262144 131072; do
+        timeout -k 10 300 python -u bench.py --envs $N --steps 400 --warmup 30 --no-cpu-baseline > $O/shard_$N.json 2> $O/shard_$N.err || { tail -20 $O/shard_$N.err; exit 1; }
+        python tools/bench_line.py $O/shard_$N.json
+      done ;;
+    profile:*)
+      timeout -k 10 1500 bash tools/gpu_profile.sh $TAG ${S#profile:} > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
+      tail -5 $O/profile.log ;;
+    stamps:*)
+      python -c "from pgtg_amd.build import build; build(variant='stamps')" || exit 1
+      timeout -k 10 300 python tools/stamps.py ${S#stamps:} > $O/stamps.log 2>&1 || { tail -20 $O/stamps.log; exit 1; }
+      cat $O/stamps.log ;;
+    ab:*)
+      R=${S#ab:}; W=${R%%:*}; L=${R#*:}
+      timeout -k 10 900 bash tools/ab_multi.sh $W 3 new $L > $O/ab_$W.log 2>&1 || { tail -20 $O/ab_$W.log; exit 1; }
+      cat $O/ab_$W.log ;;
+    *) echo "unknown step $S"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
