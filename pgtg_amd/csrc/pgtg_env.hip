@@ -153,6 +153,13 @@ __device__ __forceinline__ void rec_store(EnvRec* r, uint64_t i, const EnvView& 
   r[i] = e;
 }
 
+// Tiles >= nt of a plan word (two u16 tiles per word) are padding, stored as 0 so that the device
+// state is a function of the seeds alone (LDS plan rows may hold stale bytes there).
+__device__ __forceinline__ uint32_t plan_word_mask(const DevCfg& c, int word) {
+  const int t0 = 2 * word;
+  return t0 + 1 < c.nt ? ~0u : (t0 < c.nt ? 0xffffu : 0u);
+}
+
 // Per-lane LDS view of the env's tile plan.  Lane stride is an odd number of dwords so that 64
 // lanes reading the same tile index hit distinct banks.
 struct Plan {
@@ -2079,7 +2086,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       for (int k = 0; k < c.plan_stride / 8; k++) {
         uint32_t wv[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) wv[j] = (k * 4 + j < L.plan_stride_dw) ? pw[k * 4 + j] : 0u;
+        for (int j = 0; j < 4; j++) wv[j] = (k * 4 + j < L.plan_stride_dw) ? pw[k * 4 + j] & plan_word_mask(c, k * 4 + j) : 0u;
         dstp[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
       }
       xw[0] = ((uint32_t)vv.px & 0xffffu) | ((uint32_t)vv.py << 16);
@@ -2112,7 +2119,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     for (int k = 0; k < c.plan_stride / 8; k++) {
       uint32_t wv[4];
 #pragma unroll
-      for (int j = 0; j < 4; j++) wv[j] = (k * 4 + j < L.plan_stride_dw) ? plan_w[k * 4 + j] : 0u;
+      for (int j = 0; j < 4; j++) wv[j] = (k * 4 + j < L.plan_stride_dw) ? plan_w[k * 4 + j] & plan_word_mask(c, k * 4 + j) : 0u;
       dstp[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
     }
   }
@@ -2194,7 +2201,7 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
   for (int q = 0; q < pwords / 4; q++) {
     uint32_t wv[4];
 #pragma unroll
-    for (int j = 0; j < 4; j++) wv[j] = (q * 4 + j < pdw) ? pw[q * 4 + j] : 0u;
+    for (int j = 0; j < 4; j++) wv[j] = (q * 4 + j < pdw) ? (pw[q * 4 + j] & plan_word_mask(c, q * 4 + j)) : 0u;
     d4[q] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
   }
   d4[pwords / 4] = make_uint4(((uint32_t)px & 0xffffu) | ((uint32_t)py << 16),
