@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PGTG_ABI_VERSION 3
+#define PGTG_ABI_VERSION 4
 
 /* status codes (Python facade maps them to the reference's exception types) */
 #define PGTG_OK 0
@@ -41,10 +41,10 @@ extern "C" {
 #define PGTG_E_MAP -5          /* map without route / no start square / empty route choice      */
 
 /* limits of this build */
-#define PGTG_MAX_TILES 64      /* width*height of the tile map */
-#define PGTG_MAX_CHANNELS 48
-#define PGTG_MAX_RULES 8
-#define PGTG_MAX_WINDOW 15     /* observation window side (9 fixed, 2*s+1 sliding) */
+#define PGTG_MAX_TILES 256     /* width*height of the tile map (16 x 16; traffic: squares <= 255 per side) */
+#define PGTG_MAX_CHANNELS 48   /* observation keys (the reference's feature vocabulary has 51 distinct names) */
+#define PGTG_MAX_RULES 8       /* traffic rules: the triggered-rule mask output is one byte per env */
+#define PGTG_MAX_WINDOW 31     /* observation window side (9 fixed, 2*s+1 sliding, s <= 15) */
 
 /* observation channel codes (one per key of the reference's obs["map"] dict) */
 enum {
@@ -140,7 +140,7 @@ typedef struct {
   int32_t terminated, flat_tire, phase, elapsed;
   int32_t n_cars, next_car_id, path_len, error;
   uint32_t spawn_counter;
-  uint64_t seed, used_subgoals;
+  uint64_t seed, used_subgoals;       /* bit t: tile t's subgoal used (tiles 0..63) */
   int32_t n_spawners, car_tail;        /* car slots in use (cars + empty slots before the last car) */
 } PgtgEnvState;
 

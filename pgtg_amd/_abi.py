@@ -14,8 +14,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 # PGTG_LIB selects another build of the same library (test variants, pgtg_amd/build.py VARIANTS)
 LIB_PATH = os.environ.get("PGTG_LIB") or os.path.join(PKG, "libpgtg_hip.so")
 
-PGTG_ABI_VERSION = 3
-MAX_TILES = 64
+PGTG_ABI_VERSION = 4
+MAX_TILES = 256
 MAX_CHANNELS = 48
 MAX_RULES = 8
 

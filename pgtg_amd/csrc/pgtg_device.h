@@ -11,10 +11,11 @@ namespace pgtg {
 
 constexpr int kTile = 9;
 constexpr int kMaxTiles = PGTG_MAX_TILES;
-constexpr int kMaxEdges = 256;    // directed interior edges of a <=64-tile grid (<= 224)
+constexpr int kSmallTiles = 64;   // maps of <= 64 tiles: u64 tile masks, edge table and rewards in LDS
+constexpr int kMaxEdges = 1024;   // directed interior edges of a <= 256-tile grid (<= 960)
+constexpr int kSmallEdges = 256;  // directed interior edges of a <= 64-tile grid (<= 224): the LDS edge table
 constexpr int kMaxBorder = 192;   // border-connection candidates (<= 2w+2h-2)
 constexpr int kMaxWin = PGTG_MAX_WINDOW;
-constexpr int kMaskWords = (kMaxWin * kMaxWin + 31) / 32;  // 8
 constexpr int kBlock = 256;       // lanes (= envs) per workgroup for the step kernels
 constexpr int kSpCache = 24;      // spawner-list entries k_env keeps in LDS (the rest are read from HBM)
 
@@ -30,16 +31,19 @@ constexpr uint32_t SQ_WALL = 1u << 0, SQ_SUBGOAL = 1u << 1, SQ_USED = 1u << 2, S
                    SQ_TLIGHT = 1u << 8, SQ_SPAWNER = 1u << 9;
 
 // Tile-plan entry (u16): bits 0-3 exits (N,E,S,W), 4-6 obstacle type (0 none, 1 ice, 2 broken
-// road, 3 sand, 4 traffic light), 7-10 obstacle mask id, 11-13 subgoal exit direction + 1.
+// road, 3 sand, 4 traffic light), 7-10 obstacle mask id, 11-13 subgoal exit direction + 1, 14 the
+// tile's subgoal is used (maps of > 64 tiles; smaller maps keep the used tiles in EnvRec's u64).
+constexpr uint32_t kPlanUsed = 1u << 14;
 __host__ __device__ inline uint32_t plan_exits(uint32_t p) { return p & 15u; }
 __host__ __device__ inline uint32_t plan_otype(uint32_t p) { return (p >> 4) & 7u; }
 __host__ __device__ inline uint32_t plan_omask(uint32_t p) { return (p >> 7) & 15u; }
 __host__ __device__ inline int plan_sgdir(uint32_t p) { return (int)((p >> 11) & 7u) - 1; }
 
 // EnvRec (32 B, one uint4 pair per env):
-//  w0 = px | py<<16 (int16)   w1 = vx | vy<<16 (int16)   w2 = phase | flags<<16 | path_len<<24
+//  w0 = px | py<<16 (int16)   w1 = vx | vy<<16 (int16)   w2 = phase | flags<<16 (4 bits) | path_len<<20
 //  w3 = elapsed steps         w4 = start_tile | start_dir<<8 | goal_tile<<16 | goal_dir<<24
-//  w5 = spawn counter (SeedSequence children spawned)   w6,w7 = used-subgoal tile mask (u64)
+//  w5 = spawn counter (SeedSequence children spawned)   w6,w7 = used-subgoal tile mask (u64; maps of <= 64
+//  tiles, larger maps mark the plan words, kPlanUsed)
 struct EnvRec {
   uint4 a, b;
 };
@@ -51,8 +55,7 @@ struct DevCfg {
   uint32_t fixed_sg;
   int32_t start_mode, goal_mode, sx, sy, sdir, gx, gy, gdir, min_distance;
   int32_t n_edges, keep;
-  uint64_t h0[4];  // full-grid exit masks (N, E, S, W) before removals
-  uint8_t ea[kMaxEdges], eb[kMaxEdges], ed[kMaxEdges], erev[kMaxEdges];
+  uint64_t h0[4][4];  // full-grid exit masks (N, E, S, W) before removals, 4 x 64 tiles
   int32_t n_border, n_border_add;
   uint8_t bt[kMaxBorder], bd[kMaxBorder];
   double obstacle_probability;
@@ -101,10 +104,10 @@ struct Tables {
   uint32_t seg[4][3];       // kExitSeg
   uint32_t obst[14][3];     // kObstMask
   uint32_t spawner[16][3];  // kLaneSpawner
-  double ind[kMaxTiles + 1];  // sum_subgoals_reward / num_subgoals
-  // removable edges in graph-theory order, oriented: a | b<<8 | d<<16 | reverse edge<<24 with a the
-  // north/west tile and d 1 (east) or 2 (south)
-  uint32_t epk[kMaxEdges];
+  double ind[kSmallTiles + 1];  // sum_subgoals_reward / num_subgoals (longer paths: DevCfg::ind_reward)
+  // removable edges in graph-theory order, oriented: a | b<<8 | horizontal<<16 | reverse edge<<17 with
+  // a the north/west tile (maps of <= 64 tiles; larger maps read DevState::epk)
+  uint32_t epk[kSmallEdges];
   uint8_t bt[kMaxBorder], bd[kMaxBorder];
   // observation channel codes (DevCfg::channels as bytes): read per lane when the lanes of a group
   // build different channels of one env's image (a per-lane index into the DevCfg block would be a
@@ -167,6 +170,7 @@ struct DevState {
   unsigned long long* wg_ticks;  // [1]: wall-clock ticks of workgroup 0 in the last launch (start offsets)
   const int8_t* nsd_tab;
   const int8_t* cmp_tab;
+  const uint32_t* epk;    // [n_edges] the Tables::epk edge table of maps of > 64 tiles (global memory)
 };
 
 // ------------------------------------------------------------------------------------------------

@@ -66,21 +66,23 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// One env's tile plan (plan_stride u16 words in HBM, a multiple of 8, <= 64) into its LDS row of
-// pdw words, all loads first.
+// One env's tile plan (plan_stride u16 words in HBM, a multiple of 8) into its LDS row of pdw words,
+// in blocks of 8 x 16 bytes (one block for maps of <= 64 tiles), each block's loads first.
 __device__ __forceinline__ void stage_plan(const uint16_t* __restrict__ plan, int plan_stride, uint32_t* dst, int pdw) {
   const uint4* src = reinterpret_cast<const uint4*>(plan);
   const int nq = plan_stride / 8;
-  uint4 q[8];
+  for (int k0 = 0; k0 < nq; k0 += 8) {
+    uint4 q[8];
 #pragma unroll
-  for (int k = 0; k < 8; k++) q[k] = src[k < nq ? k : 0];  // unconditional: registers, not scratch
+    for (int k = 0; k < 8; k++) q[k] = src[k0 + k < nq ? k0 + k : k0];  // unconditional: registers, not scratch
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    if (k < nq) {
-      const uint32_t wv[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+    for (int k = 0; k < 8; k++) {
+      if (k0 + k < nq) {
+        const uint32_t wv[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (k * 4 + j < pdw) dst[k * 4 + j] = wv[j];
+        for (int j = 0; j < 4; j++)
+          if ((k0 + k) * 4 + j < pdw) dst[(k0 + k) * 4 + j] = wv[j];
+      }
     }
   }
 }
@@ -132,8 +134,8 @@ __device__ __forceinline__ EnvView rec_load(const EnvRec* r, uint64_t i) {
   v.vx = (int)(int16_t)(e.a.y & 0xffffu);
   v.vy = (int)(int16_t)(e.a.y >> 16);
   v.phase = e.a.z & 0xffffu;
-  v.flags = (e.a.z >> 16) & 0xffu;
-  v.path_len = e.a.z >> 24;
+  v.flags = (e.a.z >> 16) & 0xfu;
+  v.path_len = e.a.z >> 20;
   v.elapsed = e.a.w;
   v.sg = e.b.x;
   v.spawn = e.b.y;
@@ -144,7 +146,7 @@ __device__ __forceinline__ void rec_store(EnvRec* r, uint64_t i, const EnvView& 
   EnvRec e;
   e.a.x = ((uint32_t)v.px & 0xffffu) | ((uint32_t)v.py << 16);
   e.a.y = ((uint32_t)v.vx & 0xffffu) | ((uint32_t)v.vy << 16);
-  e.a.z = (v.phase & 0xffffu) | ((v.flags & 0xffu) << 16) | (v.path_len << 24);
+  e.a.z = (v.phase & 0xffffu) | ((v.flags & 0xfu) << 16) | (v.path_len << 20);
   e.a.w = v.elapsed;
   e.b.x = v.sg;
   e.b.y = v.spawn;
@@ -159,6 +161,16 @@ __device__ __forceinline__ uint32_t plan_word_mask(const DevCfg& c, int word) {
   const int t0 = 2 * word;
   return t0 + 1 < c.nt ? ~0u : (t0 < c.nt ? 0xffffu : 0u);
 }
+// The env's LDS plan row (pdw words) back to its HBM tile plan (plan_stride u16 words), padding as 0.
+__device__ __forceinline__ void store_plan_row(const DevCfg& c, const DevState& S, uint64_t i, const uint32_t* pw, int pdw) {
+  uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
+  for (int k = 0; k < c.plan_stride / 8; k++) {
+    uint32_t wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) wv[j] = (k * 4 + j < pdw) ? pw[k * 4 + j] & plan_word_mask(c, k * 4 + j) : 0u;
+    dstp[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+  }
+}
 
 // Per-lane LDS view of the env's tile plan.  Lane stride is an odd number of dwords so that 64
 // lanes reading the same tile index hit distinct banks.
@@ -167,7 +179,15 @@ struct Plan {
   __device__ __forceinline__ uint32_t operator[](int t) const { return p[t]; }
 };
 
+// Has tile t's subgoal been used (EpisodeMap.set_subgoals_to_used, pgtg/map.py:143-171)?  p = the
+// tile's plan word: maps of > 64 tiles (BIG) mark it there, smaller maps in the u64 of EnvRec.
+template <bool BIG>
+__device__ __forceinline__ bool used_bit(const EnvView& v, uint32_t p, int t) {
+  return BIG ? (p & kPlanUsed) != 0u : ((v.used >> t) & 1ull) != 0ull;
+}
+
 // features of square (x, y) inside the map (pgtg/parser.py:47-155 semantics, see file header)
+template <bool BIG>
 __device__ __forceinline__ uint32_t square_flags(const DevCfg& c, const Plan& pl, const EnvView& v, int x, int y) {
   int tx = x / kTile, ty = y / kTile;
   int lx = x - tx * kTile, ly = y - ty * kTile;
@@ -180,7 +200,7 @@ __device__ __forceinline__ uint32_t square_flags(const DevCfg& c, const Plan& pl
   if (wall) f |= SQ_WALL;
   int d = seg_dir(lx, ly);
   if (d >= 0 && ((ex >> d) & 1u)) {
-    if (plan_sgdir(p) == d) f |= ((v.used >> t) & 1ull) ? SQ_USED : SQ_SUBGOAL;
+    if (plan_sgdir(p) == d) f |= used_bit<BIG>(v, p, t) ? SQ_USED : SQ_SUBGOAL;
     if ((int)(v.sg & 0xffu) == t && (int)((v.sg >> 8) & 0xffu) == d) f |= SQ_START;
     if ((int)((v.sg >> 16) & 0xffu) == t && (int)(v.sg >> 24) == d) f |= SQ_FINAL;
   }
@@ -320,7 +340,117 @@ __device__ __forceinline__ int rand_dir(const DevCfg& c, Pcg& r, int x, int y) {
   return __ffs((int)m) - 1;
 }
 
-// 256-bit set kept in four named registers (no private-array indexing -> no scratch)
+// ------------------------------------------------------------------------------------------------
+// tile masks: uint32_t (<= 32 tiles), uint64_t (<= 64) or Bits<4> (<= 256 tiles, 16 x 16 maps).  The
+// generator and the path compiler are written once over these helpers; Bits keeps its words in named
+// registers (every index is resolved with selects: no private-array indexing, no scratch).
+// ------------------------------------------------------------------------------------------------
+template <int NW>
+struct Bits {
+  uint64_t w[NW];
+};
+template <int NW>
+__device__ __forceinline__ Bits<NW> operator|(Bits<NW> a, const Bits<NW>& b) {
+#pragma unroll
+  for (int q = 0; q < NW; q++) a.w[q] |= b.w[q];
+  return a;
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW> operator&(Bits<NW> a, const Bits<NW>& b) {
+#pragma unroll
+  for (int q = 0; q < NW; q++) a.w[q] &= b.w[q];
+  return a;
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW> operator~(Bits<NW> a) {
+#pragma unroll
+  for (int q = 0; q < NW; q++) a.w[q] = ~a.w[q];
+  return a;
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW>& operator|=(Bits<NW>& a, const Bits<NW>& b) { return a = a | b; }
+template <int NW>
+__device__ __forceinline__ Bits<NW>& operator&=(Bits<NW>& a, const Bits<NW>& b) { return a = a & b; }
+// shifts by 0 <= n < 64 (grid rows of <= 16 tiles, single columns)
+template <int NW>
+__device__ __forceinline__ Bits<NW> operator<<(const Bits<NW>& a, int n) {
+  Bits<NW> r;
+#pragma unroll
+  for (int q = 0; q < NW; q++) r.w[q] = (a.w[q] << n) | (q > 0 && n ? a.w[q - 1] >> (64 - n) : 0ull);
+  return r;
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW> operator>>(const Bits<NW>& a, int n) {
+  Bits<NW> r;
+#pragma unroll
+  for (int q = 0; q < NW; q++) r.w[q] = (a.w[q] >> n) | (q + 1 < NW && n ? a.w[q + 1] << (64 - n) : 0ull);
+  return r;
+}
+__device__ __forceinline__ bool mask_any(uint32_t m) { return m != 0u; }
+__device__ __forceinline__ bool mask_any(uint64_t m) { return m != 0ull; }
+template <int NW>
+__device__ __forceinline__ bool mask_any(const Bits<NW>& m) {
+  uint64_t o = 0;
+#pragma unroll
+  for (int q = 0; q < NW; q++) o |= m.w[q];
+  return o != 0ull;
+}
+template <typename M>
+__device__ __forceinline__ bool mask_eq(const M& a, const M& b) { return !mask_any((a & ~b) | (b & ~a)); }
+__device__ __forceinline__ bool mask_get(uint32_t m, int t) { return (m >> t) & 1u; }
+__device__ __forceinline__ bool mask_get(uint64_t m, int t) { return (m >> t) & 1ull; }
+template <int NW>
+__device__ __forceinline__ bool mask_get(const Bits<NW>& m, int t) {
+  uint64_t x = 0;
+#pragma unroll
+  for (int q = 0; q < NW; q++) x = (t >> 6) == q ? m.w[q] : x;
+  return (x >> (t & 63)) & 1ull;
+}
+template <typename M>
+__device__ __forceinline__ M mask_bit(int t) {
+  return (M)1 << t;
+}
+template <>
+__device__ __forceinline__ Bits<4> mask_bit<Bits<4>>(int t) {
+  Bits<4> r;
+#pragma unroll
+  for (int q = 0; q < 4; q++) r.w[q] = (t >> 6) == q ? 1ull << (t & 63) : 0ull;
+  return r;
+}
+template <typename M>
+__device__ __forceinline__ M mask_zero() {
+  return (M)0;
+}
+template <>
+__device__ __forceinline__ Bits<4> mask_zero<Bits<4>>() {
+  Bits<4> r;
+#pragma unroll
+  for (int q = 0; q < 4; q++) r.w[q] = 0ull;
+  return r;
+}
+// index of the lowest set bit (m != 0)
+__device__ __forceinline__ int mask_ctz(uint32_t m) { return __ffs((int)m) - 1; }
+__device__ __forceinline__ int mask_ctz(uint64_t m) { return __ffsll((long long)m) - 1; }
+template <int NW>
+__device__ __forceinline__ int mask_ctz(const Bits<NW>& m) {
+  int r = -1;
+#pragma unroll
+  for (int q = NW - 1; q >= 0; q--) r = m.w[q] ? q * 64 + __ffsll((long long)m.w[q]) - 1 : r;
+  return r;
+}
+// the full-grid exit mask of direction d (DevCfg::h0) as an M
+template <typename M>
+__device__ __forceinline__ M mask_h0(const DevCfg& c, int d) {
+  return (M)c.h0[d][0];
+}
+template <>
+__device__ __forceinline__ Bits<4> mask_h0<Bits<4>>(const DevCfg& c, int d) {
+  Bits<4> r;
+#pragma unroll
+  for (int q = 0; q < 4; q++) r.w[q] = c.h0[d][q];
+  return r;
+}
+
 // k-th (0-based) set bit of a 64-bit word, branch-free (popcount halving)
 __device__ __forceinline__ int select64(uint64_t x, int k) {
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
@@ -395,14 +525,14 @@ __device__ __forceinline__ bool still_connected(M hN, M hE, M hS, M hW, int w, i
   // Two expansions per side between checks: the sets only grow, so meeting and exhaustion are
   // still detected (at most one expansion late) with half the loop control of a step-wise loop.
   // One exit condition keeps the loop's mask bookkeeping short.
-  M Ra = (M)1 << a, Rb = (M)1 << b;
+  M Ra = mask_bit<M>(a), Rb = mask_bit<M>(b);
   bool done, res;
   do {
     const M Ma = expand_sym<M>(Ra, hN, hE, hS, hW, w), Mb = expand_sym<M>(Rb, hN, hE, hS, hW, w);
     const M Na = expand_sym<M>(Ma, hN, hE, hS, hW, w), Nb = expand_sym<M>(Mb, hN, hE, hS, hW, w);
-    const bool meet = (Na & Nb) != 0, exa = Na == Ma, exb = Nb == Mb;
+    const bool meet = mask_any(Na & Nb), exa = mask_eq(Na, Ma), exb = mask_eq(Nb, Mb);
     const M X = exa ? Na : Nb;
-    res = meet || (((X >> s) ^ (X >> g)) & 1) == 0;
+    res = meet || mask_get(X, s) == mask_get(X, g);
     done = meet || exa || exb;
     Ra = Na;
     Rb = Nb;
@@ -411,12 +541,14 @@ __device__ __forceinline__ bool still_connected(M hN, M hE, M hS, M hW, int w, i
 }
 
 // generate_map_graph's edge-removal loop (map_generator.py:218-264) on exit masks of type M
-// (uint32_t when the map has <= 32 tiles).  removable_edges keeps graph-theory's nested-dict order
-// (host table ea/eb/ed/erev); an edge pair stays removed iff start->end stays connected, which is
-// exactly the outcome of the reference's BFS-path test + re-add.  A removed edge whose two tiles
-// still share an intact 4-cycle cannot disconnect anything; otherwise still_connected decides.
+// (uint32_t when the map has <= 32 tiles, Bits<4> beyond 64).  removable_edges keeps graph-theory's
+// nested-dict order (edge table `epk`: the LDS copy for maps of <= 64 tiles, else global memory); an
+// edge pair stays removed iff start->end stays connected, which is exactly the outcome of the
+// reference's BFS-path test + re-add.  A removed edge whose two tiles still share an intact 4-cycle
+// cannot disconnect anything; otherwise still_connected decides.
 template <typename M, int NW>
-__device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, int gl_t, M& hN, M& hE, M& hS, M& hW) {
+__device__ __forceinline__ void remove_edges(const DevCfg& c, const uint32_t* __restrict__ epk, Pcg& r, int st_t,
+                                             int gl_t, M& hN, M& hE, M& hS, M& hW) {
   // (pinned: re-loaded from the DevCfg in the loop under scalar-register pressure otherwise)
   const int w = pinned(c.tw), keep = pinned(c.keep), n_edges = pinned(c.n_edges);
   EdgeBits<NW> L;
@@ -434,8 +566,8 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, 
     L.clear(e);
     return e;
   };
-  uint32_t pk = sT.epk[draw_edge(nrem)];
-  L.clear((int)(pk >> 24));
+  uint32_t pk = epk[draw_edge(nrem)];
+  L.clear((int)(pk >> 17));
   nrem -= 2;
 #ifdef PGTG_STAMPS
   unsigned long long dbg_bfs = 0, dbg_iters = 0;
@@ -445,20 +577,21 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, 
     const bool more = nrem > 0;  // uniform: every lane is in the same iteration
     int e_next = 0;
     if (more) e_next = draw_edge(nrem);
-    const uint32_t pk_next = sT.epk[e_next];
+    const uint32_t pk_next = epk[e_next];
     // remove edge a-b (horizontal: a left of b; vertical: a above b), branch-free
     const int a = (int)(pk & 255u), b = (int)((pk >> 8) & 255u);
-    const bool hz = ((pk >> 16) & 255u) == 1u;
-    const M ma = (M)1 << a, mb = (M)1 << b, mab = ma | mb;
+    const bool hz = (pk >> 16) & 1u;
+    const M ma = mask_bit<M>(a), mb = mask_bit<M>(b), mab = ma | mb, z = mask_zero<M>();
     const M sN = hN, sE = hE, sS = hS, sW = hW;
-    hE &= ~(hz ? ma : (M)0);
-    hW &= ~(hz ? mb : (M)0);
-    hS &= ~(hz ? (M)0 : ma);
-    hN &= ~(hz ? (M)0 : mb);
+    hE &= ~(hz ? ma : z);
+    hW &= ~(hz ? mb : z);
+    hS &= ~(hz ? z : ma);
+    hN &= ~(hz ? z : mb);
     // an intact unit square through a and b on either side keeps everything connected
     const M P1 = hz ? hN : hW, P2 = hz ? hS : hE, F = hz ? hE : hS;
     const int off = hz ? w : 1;
-    const bool cyc = ((P1 & mab) == mab && (F & (ma >> off))) || ((P2 & mab) == mab && (F & (ma << off)));
+    const bool cyc = (mask_eq(P1 & mab, mab) && mask_any(F & (ma >> off))) ||
+                     (mask_eq(P2 & mab, mab) && mask_any(F & (ma << off)));
     count -= 2;
 #ifdef PGTG_STAMPS
     const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
@@ -475,7 +608,7 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, Pcg& r, int st_t, 
       r = r_before;  // the reference stops drawing here
       break;
     }
-    L.clear((int)(pk_next >> 24));
+    L.clear((int)(pk_next >> 17));
     pk = pk_next;
     nrem -= 2;
   }
@@ -501,7 +634,10 @@ __device__ __forceinline__ void add_border_connections(const DevCfg& c, Pcg& r, 
 }
 
 // generate_map (map_generator.py:43-189) -> tile plan (exits + obstacles) in LDS, start/goal
-__device__ __forceinline__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* plan, int& st_t, int& st_d, int& gl_t, int& gl_d) {
+// (BIG: maps of > 64 tiles, 256-bit masks and the global edge table `epk`)
+template <bool BIG>
+__device__ __forceinline__ void generate_map(const DevCfg& c, const uint32_t* __restrict__ epk, Pcg& r, uint16_t* plan,
+                                             int& st_t, int& st_d, int& gl_t, int& gl_d) {
   const int w = c.tw;
   // chose_random_start_and_goal_position_and_direction (map_generator.py:475-571)
   int s0, s1, s2 = c.sdir, g0, g1, g2 = c.gdir;
@@ -546,23 +682,31 @@ __device__ __forceinline__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* 
   gl_d = g2;
   STAMP(13);
 
-  // generate_map_graph (map_generator.py:192-266): full grid (host masks c.h0), then removals
-  uint64_t hN, hE, hS, hW;
+  // generate_map_graph (map_generator.py:192-266): full grid (host masks c.h0), then removals;
+  // map_graph_to_tile_map_object (map_generator.py:269-334): exits straight into the LDS plan
   STAMP(14);
-  if (c.nt <= 32) {
-    uint32_t n = (uint32_t)c.h0[0], e = (uint32_t)c.h0[1], so = (uint32_t)c.h0[2], we = (uint32_t)c.h0[3];
-    if (c.n_edges <= 64) remove_edges<uint32_t, 1>(c, r, st_t, gl_t, n, e, so, we);
-    else remove_edges<uint32_t, 2>(c, r, st_t, gl_t, n, e, so, we);
-    hN = n; hE = e; hS = so; hW = we;
+  if (BIG) {
+    Bits<4> n = mask_h0<Bits<4>>(c, 0), e = mask_h0<Bits<4>>(c, 1), so = mask_h0<Bits<4>>(c, 2), we = mask_h0<Bits<4>>(c, 3);
+    remove_edges<Bits<4>, 16>(c, epk, r, st_t, gl_t, n, e, so, we);
+    for (int t = 0; t < c.nt; t++)
+      plan[t] = (uint16_t)((uint32_t)mask_get(n, t) | (uint32_t)mask_get(e, t) << 1 | (uint32_t)mask_get(so, t) << 2 |
+                           (uint32_t)mask_get(we, t) << 3);
   } else {
-    hN = c.h0[0]; hE = c.h0[1]; hS = c.h0[2]; hW = c.h0[3];
-    remove_edges<uint64_t, 4>(c, r, st_t, gl_t, hN, hE, hS, hW);
+    uint64_t hN, hE, hS, hW;
+    if (c.nt <= 32) {
+      uint32_t n = (uint32_t)c.h0[0][0], e = (uint32_t)c.h0[1][0], so = (uint32_t)c.h0[2][0], we = (uint32_t)c.h0[3][0];
+      if (c.n_edges <= 64) remove_edges<uint32_t, 1>(c, epk, r, st_t, gl_t, n, e, so, we);
+      else remove_edges<uint32_t, 2>(c, epk, r, st_t, gl_t, n, e, so, we);
+      hN = n; hE = e; hS = so; hW = we;
+    } else {
+      hN = c.h0[0][0]; hE = c.h0[1][0]; hS = c.h0[2][0]; hW = c.h0[3][0];
+      remove_edges<uint64_t, 4>(c, epk, r, st_t, gl_t, hN, hE, hS, hW);
+    }
+    for (int t = 0; t < c.nt; t++)
+      plan[t] = (uint16_t)((uint32_t)((hN >> t) & 1ull) | (uint32_t)((hE >> t) & 1ull) << 1 |
+                           (uint32_t)((hS >> t) & 1ull) << 2 | (uint32_t)((hW >> t) & 1ull) << 3);
   }
   STAMP(15);
-  // map_graph_to_tile_map_object (map_generator.py:269-334): exits straight into the LDS plan
-  for (int t = 0; t < c.nt; t++)
-    plan[t] = (uint16_t)((uint32_t)((hN >> t) & 1ull) | (uint32_t)((hE >> t) & 1ull) << 1 |
-                         (uint32_t)((hS >> t) & 1ull) << 2 | (uint32_t)((hW >> t) & 1ull) << 3);
   plan[st_t] |= (uint16_t)(1u << st_d);
   plan[gl_t] |= (uint16_t)(1u << gl_d);
   // add_connections_to_borders (map_generator.py:337-371), candidate list from the host
@@ -606,24 +750,25 @@ __device__ __forceinline__ void generate_map(const DevCfg& c, Pcg& r, uint16_t* 
 template <typename M>
 __device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, int s, int g) {
   const int w = c.tw;
-  M hN = 0, hE = 0, hS = 0, hW = 0;
+  M hN = mask_zero<M>(), hE = hN, hS = hN, hW = hN;
   for (int t = 0; t < c.nt; t++) {
-    const M e = (M)plan_exits(plan[t]);
-    hN |= (e & 1) << t;
-    hE |= ((e >> 1) & 1) << t;
-    hS |= ((e >> 2) & 1) << t;
-    hW |= ((e >> 3) & 1) << t;
+    const uint32_t e = plan_exits(plan[t]);
+    const M b = mask_bit<M>(t), z = mask_zero<M>();
+    hN |= (e & 1u) ? b : z;
+    hE |= (e & 2u) ? b : z;
+    hS |= (e & 4u) ? b : z;
+    hW |= (e & 8u) ? b : z;
   }
-  hN &= (M)c.h0[0];  // interior exits only: border exits lead off the map
-  hE &= (M)c.h0[1];
-  hS &= (M)c.h0[2];
-  hW &= (M)c.h0[3];
+  hN &= mask_h0<M>(c, 0);  // interior exits only: border exits lead off the map
+  hE &= mask_h0<M>(c, 1);
+  hS &= mask_h0<M>(c, 2);
+  hW &= mask_h0<M>(c, 3);
   STAMP(24);
-  M vis = (M)1 << g, front = vis;
-  M cN = 0, cE = 0, cS = 0, cW = 0;  // tiles with a neighbour one layer closer, per direction
-  while (!((vis >> s) & 1)) {
+  M vis = mask_bit<M>(g), front = vis;
+  M cN = mask_zero<M>(), cE = cN, cS = cN, cW = cN;  // tiles with a neighbour one layer closer, per direction
+  while (!mask_get(vis, s)) {
     const M nx = expand<M>(front, hN, hE, hS, hW, w) & ~vis;
-    if (!nx) return 0;
+    if (!mask_any(nx)) return 0;
     cN |= nx & hN & (front << w);
     cE |= nx & hE & (front >> 1);
     cS |= nx & hS & (front >> w);
@@ -632,21 +777,17 @@ __device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, int
     front = nx;
   }
   STAMP(25);
-  M pN = 0, pE = 0, pS = 0, pW = 0;
   int v = s, len = 1;
-  while (v != g) {
-    const M b = (M)1 << v;
-    if (cN & b) { pN |= b; v -= w; }
-    else if (cE & b) { pE |= b; v += 1; }
-    else if (cS & b) { pS |= b; v += w; }
-    else { pW |= b; v -= 1; }
+  while (v != g) {  // the walk marks the direction to the next tile on every path tile but the goal's
+    uint32_t d;
+    int nv;
+    if (mask_get(cN, v)) { d = 1u; nv = v - w; }
+    else if (mask_get(cE, v)) { d = 2u; nv = v + 1; }
+    else if (mask_get(cS, v)) { d = 3u; nv = v + w; }
+    else { d = 4u; nv = v - 1; }
+    plan[v] = (uint16_t)((plan[v] & ~(7u << 11)) | d << 11);
+    v = nv;
     len++;
-  }
-  for (M m = pN | pE | pS | pW; m; m &= m - 1) {
-    const int t = __builtin_ctzll((uint64_t)m);
-    const M b = (M)1 << t;
-    const uint32_t d = (pN & b) ? 1u : (pE & b) ? 2u : (pS & b) ? 3u : 4u;
-    plan[t] = (uint16_t)((plan[t] & ~(7u << 11)) | d << 11);
   }
   return len;
 }
@@ -858,7 +999,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
 }
 
 // The full per-env reset.  `key` = spawn counter (5 children per episode).  Returns 0 or -code.
-template <bool TR>
+template <bool TR, bool BIG>
 __device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, uint16_t* plan,
                                          TrafState& ts) {
   STAMP(8);
@@ -881,11 +1022,12 @@ __device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uin
     gl_t = (int)((c.fixed_sg >> 16) & 0xffu);
     gl_d = (int)(c.fixed_sg >> 24);
   } else {
-    generate_map(c, map_rng, plan, st_t, st_d, gl_t, gl_d);
+    generate_map<BIG>(c, BIG ? S.epk : sT.epk, map_rng, plan, st_t, st_d, gl_t, gl_d);
   }
   v.sg = (uint32_t)st_t | (uint32_t)st_d << 8 | (uint32_t)gl_t << 16 | (uint32_t)gl_d << 24;
   STAMP(10);
-  int len = c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t);
+  int len = BIG ? compile_path<Bits<4>>(c, plan, st_t, gl_t)
+          : (c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t));
   STAMP(11);
   v.used = 0;
   v.path_len = (uint32_t)len;
@@ -953,6 +1095,7 @@ struct ObsInfo {
 };
 
 // nearest subgoal / final goal square from (x, y): min Manhattan, x-major first (environment.py:1471-1480)
+template <bool BIG>
 __device__ __forceinline__ bool nearest_goal_square(const DevCfg& c, const Plan& pl, const EnvView& v, int x, int y, int& bx, int& by) {
   int best = 0x7fffffff;
   bool found = false;
@@ -961,7 +1104,7 @@ __device__ __forceinline__ bool nearest_goal_square(const DevCfg& c, const Plan&
     uint32_t p = pl[t];
     int d = -1;
     int sd = plan_sgdir(p);
-    if (sd >= 0 && !((v.used >> t) & 1ull)) d = sd;
+    if (sd >= 0 && !used_bit<BIG>(v, p, t)) d = sd;
     for (int pass = 0; pass < 2; pass++) {
       int dd = pass == 0 ? d : (t == gl_t ? gl_d : -1);
       if (dd < 0) continue;
@@ -1028,7 +1171,7 @@ struct BitSink {
 // the window's squares row-major over x, then y.
 // Channels [ch_lo, ch_hi) only (default all) when the lanes of a group share one env's image (the
 // group's sinks merge at their shared words); `head`: also the next-subgoal direction.
-template <bool TR>
+template <bool TR, bool BIG>
 __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
                                           uint32_t* img, uint32_t bit0, ObsInfo& oi, const uint8_t* occ,
                                           int ch_lo = 0, int ch_hi = -1, bool head = true, bool lane_codes = false) {
@@ -1055,7 +1198,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
     uint32_t ex = plan_exits(p);
     uint32_t W3[3], SG[3] = {0, 0, 0}, US[3] = {0, 0, 0}, FI[3] = {0, 0, 0}, ST[3] = {0, 0, 0}, OB[3] = {0, 0, 0};
     int sd = plan_sgdir(p);
-    bool used = (v.used >> t) & 1ull;
+    bool used = used_bit<BIG>(v, p, t);
     int st_t = (int)(v.sg & 0xffu), st_d = (int)((v.sg >> 8) & 0xffu);
     int gl_t = (int)((v.sg >> 16) & 0xffu), gl_d = (int)(v.sg >> 24);
     uint32_t ot = plan_otype(p);
@@ -1142,7 +1285,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
             uint32_t f, lanes = 0;
             bool sp = false;
             if (inside(c, x, y)) {
-              f = square_flags(c, pl, v, x, y);
+              f = square_flags<BIG>(c, pl, v, x, y);
               if (code == PGTG_CH_SPAWNER) sp = square_spawner(c, pl, x, y);
               if (code >= PGTG_CH_LANE0) lanes = square_lanes(c, pl, x, y);
             } else {
@@ -1165,7 +1308,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
     int nsd = sd >= 0 ? sd : (t == gl_t ? (int)(v.sg >> 24) : -1);
     if (nsd == -1 || c.sliding) {
       int bx = 0, by = 0;
-      if (nearest_goal_square(c, pl, v, pix, piy, bx, by))
+      if (nearest_goal_square<BIG>(c, pl, v, pix, piy, bx, by))
         nsd = S.nsd_tab[(bx - pix + c.nsd_off) * c.nsd_pitch + (by - piy + c.nsd_off)];
     }
     oi.nsd = nsd;
@@ -1431,6 +1574,7 @@ __device__ __forceinline__ BrakeQuery braking_query(const DevCfg& c, const EnvVi
   return q;
 }
 // returns the mask of triggered rules (TrafficRuleEngine.evaluate_all_rules, rule_triggers)
+template <bool BIG>
 __device__ __forceinline__ uint32_t braking_decide(const DevCfg& c, const DevState& S, const EnvView& v,
                                                    const Plan& pl, const BrakeQuery& q, const uint8_t* hist) {
   if (!q.cand) return 0u;
@@ -1438,7 +1582,7 @@ __device__ __forceinline__ uint32_t braking_decide(const DevCfg& c, const DevSta
   int dir;
   int bx = 0, by = 0;
   int cp = -1;
-  if (nearest_goal_square(c, pl, v, v.px, v.py, bx, by))
+  if (nearest_goal_square<BIG>(c, pl, v, v.px, v.py, bx, by))
     cp = S.cmp_tab[(bx - v.px + c.cmp_off) * c.cmp_pitch + (by - v.py + c.cmp_off)];
   if (cp >= 0) dir = cp >> 1;  // N,NE -> south_to_north; E,SE -> west_to_east; S,SW; W,NW
   else dir = q.s2 == 0 ? 4 : 5;  // "stationary" (speed < 0.1) / "near_goal"
@@ -1456,14 +1600,16 @@ __device__ __forceinline__ uint32_t braking_decide(const DevCfg& c, const DevSta
 struct StepResult {
   double reward, cost;
   uint32_t triggered;  // traffic rules that triggered braking (bit r = rule r)
+  bool plan_dirty;     // BIG maps: a subgoal was marked used in the LDS plan (write the row back)
 };
 
-template <bool TR>
+template <bool TR, bool BIG>
 __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, const Plan& pl,
                                         int action, StepResult& res, uint8_t* occ, bool& occ_sat, const uint16_t* sp,
                                         TrafState& ts, uint8_t* hist) {
   res.reward = 0.0;
   res.cost = 0.0;
+  res.plan_dirty = false;
   if (v.flags & (kFlagTerminated | kFlagTruncated)) return PGTG_E_DONE;
   if ((unsigned)action > 8u) return PGTG_E_INVALID;
   v.phase = (v.phase + 1u) % (uint32_t)c.phase_total;
@@ -1488,7 +1634,7 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
   v.vx += ax;
   v.vy += ay;
   v.flags &= ~kFlagBraking;
-  res.triggered = (TR && c.n_rules > 0) ? braking_decide(c, S, v, pl, bq, hist) : 0u;
+  res.triggered = (TR && c.n_rules > 0) ? braking_decide<BIG>(c, S, v, pl, bq, hist) : 0u;
   if (res.triggered) {  // environment.py:1145
     v.vx = v.vy = 0;
     v.flags |= kFlagBraking;
@@ -1512,7 +1658,7 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
   const int gl_t = (int)((v.sg >> 16) & 0xffu), gl_d = (int)(v.sg >> 24);
   const int color = phase_color(c, v.phase);
   // the subgoal reward of this episode's path (one read for every subgoal the step may cross)
-  const double ind_pl = sT.ind[v.path_len];
+  const double ind_pl = BIG ? c.ind_reward[v.path_len] : sT.ind[v.path_len];
   // Without obstacle effects or cars a step's path depends on the velocity alone, so the squares
   // of kPathChunk parts are looked up together (one LDS latency per chunk instead of per part) and
   // then walked in order.  A subgoal tile marked used earlier in the same step is tested against
@@ -1547,7 +1693,7 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
     uint32_t F[kPathChunk + 1];
 #pragma unroll
     for (int j = 0; j <= kPathChunk; j++)
-      F[j] = square_flags(c, pl, v, min(max(X[j], 0), c.W - 1), min(max(Y[j], 0), c.H - 1));
+      F[j] = square_flags<BIG>(c, pl, v, min(max(X[j], 0), c.W - 1), min(max(Y[j], 0), c.H - 1));
     bool go = true;
 #pragma unroll
     for (int j = 0; j < kPathChunk; j++) {
@@ -1567,9 +1713,14 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
           go = false;
         } else {
           const int t = (y / kTile) * c.tw + x / kTile;
-          if ((f & SQ_SUBGOAL) && !((v.used >> t) & 1ull)) {
+          if ((f & SQ_SUBGOAL) && !used_bit<BIG>(v, pl[t], t)) {
             if (c.separate_cost) perf += ind_pl; else reward += ind_pl;
-            v.used |= 1ull << t;
+            if (BIG) {
+              pl.p[t] |= (uint16_t)kPlanUsed;
+              res.plan_dirty = true;
+            } else {
+              v.used |= 1ull << t;
+            }
           }
           if (k == n) {
             go = false;
@@ -1607,8 +1758,8 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
     const int nx = cx + pxp, ny = cy + pyp;
     const int ccx = min(max(cx, 0), c.W - 1), ccy = min(max(cy, 0), c.H - 1);
     const int cnx = min(max(nx, 0), c.W - 1), cny = min(max(ny, 0), c.H - 1);
-    const uint32_t f_here = square_flags(c, pl, v, ccx, ccy);
-    const uint32_t f_next = square_flags(c, pl, v, cnx, cny);
+    const uint32_t f_here = square_flags<BIG>(c, pl, v, ccx, ccy);
+    const uint32_t f_next = square_flags<BIG>(c, pl, v, cnx, cny);
     int occ_here = 0;
     if (TR && c.need_car) occ_here = occ_at(c, pl, occ, ccx, ccy);
     // crash: outside, wall (cars: traffic pass)
@@ -1632,7 +1783,13 @@ __device__ __forceinline__ int env_step(const DevCfg& c, const DevState& S, uint
     if (f & SQ_SUBGOAL) {
       if (c.separate_cost) perf += ind_pl; else reward += ind_pl;
       // set_subgoals_to_used: the flood fill covers exactly this tile's subgoal segment
-      v.used |= 1ull << ((cy / kTile) * c.tw + cx / kTile);
+      const int t = (cy / kTile) * c.tw + cx / kTile;
+      if (BIG) {
+        pl.p[t] |= (uint16_t)kPlanUsed;
+        res.plan_dirty = true;
+      } else {
+        v.used |= 1ull << t;
+      }
     }
     if (k == n) break;
     // red light at the next square (phase after this tick's increment)
@@ -1861,7 +2018,7 @@ __device__ __forceinline__ void write_small_outputs(const DevCfg& c, const PgtgO
 
 // Observation pass over sub-batches: build the envs with want != 0 (small outputs as final or not)
 // into the segment image, then write the image slice to dst (selection sel).
-template <bool TR>
+template <bool TR, bool BIG>
 __device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
                                          const PgtgOutputs& o, uint8_t* dst, uint64_t env0, int nb, bool want,
                                          bool final, const uint8_t* sel, uint32_t* st, const Lds& L,
@@ -1870,7 +2027,7 @@ __device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, con
     const int cnt = min(L.sub_envs, nb - sb);
     if (want && slot >= sb && slot < sb + cnt) {
       ObsInfo oi;
-      build_obs<TR>(c, S, pl, v, st, (uint32_t)(slot - sb) * (uint32_t)c.obs_bytes, oi, occ);
+      build_obs<TR, BIG>(c, S, pl, v, st, (uint32_t)(slot - sb) * (uint32_t)c.obs_bytes, oi, occ);
       write_small_outputs(c, o, env0 + slot, v, oi, final);
     }
     lds_barrier();
@@ -1903,7 +2060,7 @@ __device__ __forceinline__ void stagger_record(const Lds& L, const DevState& S, 
   if (L.stagger && blockIdx.x == 0 && threadIdx.x == 0) S.wg_ticks[0] = wall_clock64() - t0;
 }
 
-template <bool TR>
+template <bool TR, bool BIG>
 __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
                                                  DevState S, const uint8_t* __restrict__ actions,
                                                  const uint8_t* __restrict__ mask, PgtgOutputs out, int mode, Lds L,
@@ -2000,8 +2157,10 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (live) {
     if (mode == MODE_STEP) {
       StepResult res{0.0, 0.0, 0u};
-      if (!err) err = env_step<TR>(c, S, i, v, pl, act, res, occ, occ_sat, sp_l, ts, hist);
+      if (!err) err = env_step<TR, BIG>(c, S, i, v, pl, act, res, occ, occ_sat, sp_l, ts, hist);
       const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
+      // BIG maps keep the used subgoals in the plan: the row goes back to HBM unless the env resets now
+      if (BIG && res.plan_dirty && !(done && c.autoreset && err == 0)) store_plan_row(c, S, i, plan_w, L.plan_stride_dw);
       if (out.reward) out.reward[i] = res.reward;
       if (out.cost) out.cost[i] = res.cost;
       if (out.terminated) out.terminated[i] = (v.flags & kFlagTerminated) ? 1 : 0;
@@ -2050,7 +2209,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (single) {
     if (live && (my_sel != 2)) {
       ObsInfo oi;
-      build_obs<TR>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, occ);
+      build_obs<TR, BIG>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, occ);
       write_small_outputs(c, out, i, v, oi, my_sel == 1);
     }
     if (L.compact && reset_now) xf[0] = v.spawn;  // after the terminal image read the counters
@@ -2060,7 +2219,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     if (want_final && out.final_obs && !helpers)
       write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, -1, kBlock, lm);
   } else {
-    if (want_final) obs_pass<TR>(c, S, pl, v, out, out.final_obs, env0, nb, my_sel == 1, true, sel, st, L, occ, slot);
+    if (want_final) obs_pass<TR, BIG>(c, S, pl, v, out, out.final_obs, env0, nb, my_sel == 1, true, sel, st, L, occ, slot);
     if (L.compact) {
       if (reset_now) xf[0] = v.spawn;
       lds_barrier();
@@ -2081,14 +2240,8 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       EnvView vv{};
       vv.spawn = xw[0];
       TrafState tw{0, 0, 0, 0};
-      const int e2 = env_reset<TR>(c, S, iw, vv, reinterpret_cast<uint16_t*>(pw), tw);
-      uint4* dstp = reinterpret_cast<uint4*>(S.plan + iw * (uint64_t)c.plan_stride);
-      for (int k = 0; k < c.plan_stride / 8; k++) {
-        uint32_t wv[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) wv[j] = (k * 4 + j < L.plan_stride_dw) ? pw[k * 4 + j] & plan_word_mask(c, k * 4 + j) : 0u;
-        dstp[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-      }
+      const int e2 = env_reset<TR, BIG>(c, S, iw, vv, reinterpret_cast<uint16_t*>(pw), tw);
+      store_plan_row(c, S, iw, pw, L.plan_stride_dw);
       xw[0] = ((uint32_t)vv.px & 0xffffu) | ((uint32_t)vv.py << 16);
       xw[1] = vv.sg;
       xw[2] = vv.path_len | (uint32_t)(-e2) << 16;
@@ -2112,16 +2265,10 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       if ((TR && c.need_car) && e2 == 0) ts = TrafState{0, 0, 0, 0};
     }
   } else if (reset_now) {
-    int e2 = env_reset<TR>(c, S, i, v, pl.p, ts);
+    int e2 = env_reset<TR, BIG>(c, S, i, v, pl.p, ts);
     if (e2) err = e2;
     tr_push = (TR && c.need_car) && e2 == 0;
-    uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
-    for (int k = 0; k < c.plan_stride / 8; k++) {
-      uint32_t wv[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) wv[j] = (k * 4 + j < L.plan_stride_dw) ? plan_w[k * 4 + j] & plan_word_mask(c, k * 4 + j) : 0u;
-      dstp[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-    }
+    store_plan_row(c, S, i, plan_w, L.plan_stride_dw);
   }
   STAMP(4);
   if (live) {
@@ -2148,7 +2295,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     if (helpers && !L.compact) lds_barrier();  // the terminal observations are written before slots are rebuilt
     if (reset_now) {
       ObsInfo oi;
-      build_obs<TR>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);  // cars come from k_traffic
+      build_obs<TR, BIG>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);  // cars come from k_traffic
       write_small_outputs(c, out, i, v, oi, false);
     }
     STAMP(30);
@@ -2157,7 +2304,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     if (out.obs)
       write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr);
   } else {
-    obs_pass<TR>(c, S, pl, v, out, out.obs, env0, nb, live, false, nullptr, st, L, reset_now ? nullptr : occ,
+    obs_pass<TR, BIG>(c, S, pl, v, out, out.obs, env0, nb, live, false, nullptr, st, L, reset_now ? nullptr : occ,
                  slot);
   }
   if (mode == MODE_STEP && tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
@@ -2172,13 +2319,15 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
 // ------------------------------------------------------------------------------------------------
 // One ring entry: generate_map + compile_path + the start draw of env_reset for spawn counter `k`,
 // built in the lane's LDS plan scratch and written to HBM.
+template <bool BIG>
 __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState& S, uint64_t i, uint32_t k,
                                                 uint16_t* plan, int pdw, uint32_t* __restrict__ dst) {
   SeedPool sp = ss_pool(S.seed[i]);
   Pcg map_rng = ss_child(sp, k);
   int st_t, st_d, gl_t, gl_d;
-  generate_map(c, map_rng, plan, st_t, st_d, gl_t, gl_d);
-  const int len = c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t);
+  generate_map<BIG>(c, BIG ? S.epk : sT.epk, map_rng, plan, st_t, st_d, gl_t, gl_d);
+  const int len = BIG ? compile_path<Bits<4>>(c, plan, st_t, gl_t)
+                : (c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t));
   int px = 0, py = 0, err = 0;
   if (len == 0 || !((plan_exits(plan[st_t]) >> st_d) & 1u)) {
     err = PGTG_E_MAP;
@@ -2201,7 +2350,11 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
   for (int q = 0; q < pwords / 4; q++) {
     uint32_t wv[4];
 #pragma unroll
-    for (int j = 0; j < 4; j++) wv[j] = (q * 4 + j < pdw) ? (pw[q * 4 + j] & plan_word_mask(c, q * 4 + j)) : 0u;
+    for (int j = 0; j < 4; j++) {
+      // tiles >= nt are padding: written as 0 (the scratch holds stale LDS there), so that the queue
+      // and the plans taken from it are a function of the seeds alone (byte-identical state dumps)
+      wv[j] = (q * 4 + j < pdw) ? (pw[q * 4 + j] & plan_word_mask(c, q * 4 + j)) : 0u;
+    }
     d4[q] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
   }
   d4[pwords / 4] = make_uint4(((uint32_t)px & 0xffffu) | ((uint32_t)py << 16),
@@ -2232,6 +2385,7 @@ __device__ __forceinline__ void sub_barrier(uint32_t* ctr, uint32_t target) {
 // 4): lane e (the env's own) and lanes e + E, e + 2E, ... take a quarter of the channels each (their
 // bit sinks merge at the shared words), the env's lane also the next-subgoal direction.  `want`:
 // this lane's env needs an image.  Otherwise every env lane builds its own.
+template <bool BIG>
 __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, const EnvView& v, bool want,
                                           uint32_t* st, ObsInfo& oi, const Lds& L, int wave, int lane, bool post = true) {
   const int E = L.envs;
@@ -2252,7 +2406,7 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
     const int C = c.n_channels;
     extern __shared__ uint32_t lds[];
     const Plan pl{reinterpret_cast<uint16_t*>(lds + e * L.plan_stride_dw)};
-    build_obs<false>(c, S, pl, ve, st, (uint32_t)e * (uint32_t)c.obs_bytes, oi, nullptr, sub * C / G,
+    build_obs<false, BIG>(c, S, pl, ve, st, (uint32_t)e * (uint32_t)c.obs_bytes, oi, nullptr, sub * C / G,
                      (sub + 1) * C / G, sub == 0, true);
     STAMP(post ? 11 : 18);
     return;
@@ -2261,10 +2415,11 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
     extern __shared__ uint32_t lds[];
     const int slot = (int)threadIdx.x;
     const Plan pl{reinterpret_cast<uint16_t*>(lds + slot * L.plan_stride_dw)};
-    build_obs<false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
+    build_obs<false, BIG>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
   }
 }
 
+template <bool BIG>
 __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
                                                     DevState S, const uint8_t* __restrict__ actions, PgtgOutputs out,
                                                     Lds L) {
@@ -2342,7 +2497,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       const uint64_t ie = env0 + e;
       const uint32_t qe = xf[e * L.scratch_dw + 1];
       const uint32_t rslot = (((qe >> 2) & 3u) + (uint32_t)l) % (uint32_t)kQueueDepth;
-      gen_queue_entry(c, S, ie, xf[e * L.scratch_dw] + 5u * (uint32_t)l, gplan, pdw,
+      gen_queue_entry<BIG>(c, S, ie, xf[e * L.scratch_dw] + 5u * (uint32_t)l, gplan, pdw,
                       S.qbuf + (ie * kQueueDepth + rslot) * (uint64_t)c.qrec_dw);
     };
     for (int k = lane; k < F[0]; k += kQueueLanes) refill(k, 0);  // every empty ring's head
@@ -2368,7 +2523,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     StepResult res{0.0, 0.0, 0u};
     bool occ_sat = false;
     TrafState ts{0, 0, 0, 0};
-    err = env_step<false>(c, S, i, v, pl, act, res, nullptr, occ_sat, nullptr, ts, nullptr);
+    err = env_step<false, BIG>(c, S, i, v, pl, act, res, nullptr, occ_sat, nullptr, ts, nullptr);
     STAMP(22);
     const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
     if (out.reward) out.reward[i] = res.reward;
@@ -2377,13 +2532,14 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     if (out.truncated) out.truncated[i] = (v.flags & kFlagTruncated) ? 1 : 0;
     if (out.braking) out.braking[i] = 0;
     my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
+    if (BIG && res.plan_dirty && !my_sel) store_plan_row(c, S, i, plan_w, pdw);  // used subgoals (kPlanUsed)
     if (lm && my_sel && out.final_obs) mark_lines(lm, out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)slot, (uint32_t)c.obs_bytes);
     STAMP(23);
   }
   // the post-step image of every env (terminal for the finished ones)
   {
     ObsInfo oi;
-    group_obs(c, S, v, live, st, oi, L, wave, lane);
+    group_obs<BIG>(c, S, v, live, st, oi, L, wave, lane);
     if (live) write_small_outputs(c, out, i, v, oi, my_sel == 1);
   }
   if (env_wave) sel[slot] = my_sel;
@@ -2404,19 +2560,21 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
     // all loads of the entry first: a load after a store to S.plan (which the compiler cannot
     // tell apart from the queue) would wait for the one before it, one HBM latency per 16 bytes
-    const int nq = c.plan_stride / 8;  // 16-byte words of the tile plan (<= 8)
-    uint4 qw[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) qw[k] = q4[k < nq ? k : 0];  // unconditional: registers, not scratch
+    const int nq = c.plan_stride / 8;  // 16-byte words of the tile plan (<= 8 unless BIG)
     const uint4 meta = q4[nq];
+    for (int k0 = 0; k0 < (BIG ? nq : 1); k0 += 8) {
+      uint4 qw[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      if (k < nq) {
-        dstp[k] = qw[k];
-        const uint32_t wv[4] = {qw[k].x, qw[k].y, qw[k].z, qw[k].w};
+      for (int k = 0; k < 8; k++) qw[k] = q4[k0 + k < nq ? k0 + k : k0];  // unconditional: registers, not scratch
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-          if (k * 4 + j < pdw) plan_w[k * 4 + j] = wv[j];
+      for (int k = 0; k < 8; k++) {
+        if (k0 + k < nq) {
+          dstp[k0 + k] = qw[k];
+          const uint32_t wv[4] = {qw[k].x, qw[k].y, qw[k].z, qw[k].w};
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if ((k0 + k) * 4 + j < pdw) plan_w[(k0 + k) * 4 + j] = wv[j];
+        }
       }
     }
     const uint32_t k0 = v.spawn;
@@ -2467,7 +2625,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   STAMP(5);
   {
     ObsInfo oi;
-    group_obs(c, S, v, reset_now, st, oi, L, wave, lane, false);
+    group_obs<BIG>(c, S, v, reset_now, st, oi, L, wave, lane, false);
     if (reset_now) write_small_outputs(c, out, i, v, oi, false);
   }
   STAMP(30);
@@ -2501,7 +2659,7 @@ __global__ void __launch_bounds__(kBlock) k_gen_bench(const DevCfg* __restrict__
       Pcg g = ss_child(sp, 5u * (uint32_t)r);
       int st_t, st_d, gl_t, gl_d;
       const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-      generate_map(c, g, plan, st_t, st_d, gl_t, gl_d);
+      generate_map<false>(c, sT.epk, g, plan, st_t, st_d, gl_t, gl_d);
       const unsigned long long t1 = __builtin_amdgcn_s_memtime();
       const int len = c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t);
       const unsigned long long t2 = __builtin_amdgcn_s_memtime();
@@ -2597,7 +2755,7 @@ __global__ void __launch_bounds__(kBlock) k_squares(const DevCfg* __restrict__ c
   const Plan pl{plan_s};
   for (int q = tid; q < c.W * c.H; q += blockDim.x) {
     const int x = q / c.H, y = q - x * c.H;
-    const uint32_t f = square_flags(c, pl, v, x, y);
+    const uint32_t f = c.nt > kSmallTiles ? square_flags<true>(c, pl, v, x, y) : square_flags<false>(c, pl, v, x, y);
     uint64_t w = square_lanes(c, pl, x, y);
     if (f & SQ_WALL) w |= 1ull << 32;
     if (square_spawner(c, pl, x, y)) w |= 1ull << 37;
@@ -2710,12 +2868,22 @@ struct pgtg_handle {
   double acc_ms = 0.0;
   uint64_t acc_n = 0;
   // k_traffic: work-list parity, grid (one workgroup per CU), envs per wave in LDS, dynamic LDS
+  std::vector<uint32_t> epk;  // the map's edge table (derive_cfg): LDS copy (<= 64 tiles) or S.epk
   uint32_t tr_slot = 0;
   int kt_grid = 0, kt_cap = 16;
   int kt_plan_dw = 0, kt_rs_dw = 0;
   size_t kt_lds = 0;
 };
 
+
+// The step kernel instance a launch of `mode` runs (traffic/rules: k_env<true>; random maps without
+// them: k_envq for steps when the map queue is on, else k_env<false>; BIG: maps of > 64 tiles).
+static const void* step_fn(const pgtg_handle* h, int mode) {
+  const bool big = h->hcfg.nt > kSmallTiles;
+  if (h->hcfg.need_car || h->hcfg.n_rules > 0) return big ? (const void*)k_env<true, true> : (const void*)k_env<true, false>;
+  if (mode == MODE_STEP && h->L.queue) return big ? (const void*)k_envq<true> : (const void*)k_envq<false>;
+  return big ? (const void*)k_env<false, true> : (const void*)k_env<false, false>;
+}
 
 static thread_local std::string g_create_err;
 
@@ -2793,7 +2961,7 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
   if (in.abi_version != PGTG_ABI_VERSION) return fail(h, PGTG_E_INVALID, "ABI version mismatch");
   int tw = in.fixed_map ? in.fm_w : in.width, th = in.fixed_map ? in.fm_h : in.height;
   if (tw < 1 || th < 1) return fail(h, PGTG_E_INVALID, "map width and height must be >= 1");
-  if (tw * th > PGTG_MAX_TILES) return fail(h, PGTG_E_UNSUPPORTED, "this build supports width*height <= 64 tiles");
+  if (tw * th > PGTG_MAX_TILES) return fail(h, PGTG_E_UNSUPPORTED, "this build supports width*height <= 256 tiles");
   c.tw = tw;
   c.th = th;
   c.nt = tw * th;
@@ -2846,20 +3014,31 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
           add1(t + tw, t);
         }
       }
-    int n = 0;
+    std::vector<int> ea, eb, ed;
     for (int a : keys)
       for (int b : dst[a]) {
-        c.ea[n] = (uint8_t)a;
-        c.eb[n] = (uint8_t)b;
-        c.ed[n] = (uint8_t)(b == a - tw ? 0 : b == a + 1 ? 1 : b == a + tw ? 2 : 3);
-        n++;
+        ea.push_back(a);
+        eb.push_back(b);
+        ed.push_back(b == a - tw ? 0 : b == a + 1 ? 1 : b == a + tw ? 2 : 3);
       }
+    const int n = (int)ea.size();
+    if (n > kMaxEdges) return fail(h, PGTG_E_UNSUPPORTED, "too many map edges");
     c.n_edges = n;
-    for (int k = 0; k < 4; k++) c.h0[k] = 0;
-    for (int e = 0; e < n; e++) c.h0[c.ed[e]] |= 1ull << c.ea[e];
-    for (int e = 0; e < n; e++)
-      for (int f = 0; f < n; f++)
-        if (c.ea[f] == c.eb[e] && c.eb[f] == c.ea[e]) c.erev[e] = (uint8_t)f;
+    memset(c.h0, 0, sizeof c.h0);
+    for (int e = 0; e < n; e++) c.h0[ed[e]][ea[e] >> 6] |= 1ull << (ea[e] & 63);
+    // the edge table (Tables::epk / DevState::epk): a = north/west tile, horizontal flag, reverse edge
+    std::vector<int> pos(c.nt * 4, -1);  // (tile, direction) -> list index
+    for (int e = 0; e < n; e++) pos[ea[e] * 4 + ed[e]] = e;
+    h->epk.assign(n, 0u);
+    for (int e = 0; e < n; e++) {
+      int a = ea[e], b = eb[e], d = ed[e];
+      const int rev = pos[b * 4 + (d + 2) % 4];
+      if (d == 0 || d == 3) {  // orient: a = north/west tile, d in {E (1), S (2)}
+        std::swap(a, b);
+        d = d == 0 ? 2 : 1;
+      }
+      h->epk[e] = (uint32_t)a | (uint32_t)b << 8 | (uint32_t)(d == 1 ? 1 : 0) << 16 | (uint32_t)rev << 17;
+    }
     c.keep = (int)nearbyint((double)n * in.pct_connections);  // Python round (half to even)
   }
   // border candidates (map_generator.py:352-364)
@@ -2911,13 +3090,13 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
   c.tl_penalty = in.tl_violation_penalty;
   c.still_penalty = in.standing_still_penalty;
   c.visited_penalty = in.visited_penalty;
-  for (int k = 1; k <= kMaxTiles; k++) c.ind_reward[k] = in.sum_subgoals_reward / (double)k;
+  for (int k = 1; k <= kMaxTiles; k++) c.ind_reward[k] = in.sum_subgoals_reward / (double)k;  // fp64 like Python
   c.n_channels = in.n_channels;
   if (c.n_channels < 0 || c.n_channels > PGTG_MAX_CHANNELS) return fail(h, PGTG_E_INVALID, "bad channel count");
   c.sliding = in.sliding;
   c.ss = in.sliding_size;
   c.win = in.sliding ? 1 + 2 * in.sliding_size : kTile;
-  if (c.win < 1 || c.win > kMaxWin) return fail(h, PGTG_E_UNSUPPORTED, "observation window larger than 15");
+  if (c.win < 1 || c.win > kMaxWin) return fail(h, PGTG_E_UNSUPPORTED, "observation window larger than 31 (sliding_observation_window_size > 15)");
   c.next_subgoal = in.next_subgoal;
   c.generic_channels = 0;
   for (int k = 0; k < c.n_channels; k++) {
@@ -3119,15 +3298,15 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
   h->lds = lds_bytes(h->L);
   if (h->lds + sizeof(Tables) > 160 * 1024) return fail(h, PGTG_E_UNSUPPORTED, "LDS budget exceeded");
   if (h->lds > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)k_env<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
-    (void)hipFuncSetAttribute((const void*)k_env<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
-    (void)hipFuncSetAttribute((const void*)k_envq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+    const void* fns[] = {(const void*)k_env<true, false>, (const void*)k_env<false, false>, (const void*)k_envq<false>,
+                         (const void*)k_env<true, true>, (const void*)k_env<false, true>, (const void*)k_envq<true>};
+    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
   }
   // first-round start offsets (stagger_start) for the launches without traffic
   if (!c.need_car && c.n_rules == 0) {
     int ncu = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || ncu < 1) ncu = 256;
-    const void* fn = h->L.queue ? (const void*)k_envq : (const void*)k_env<false>;
+    const void* fn = step_fn(h, MODE_STEP);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, h->lds) != hipSuccess || per_cu < 1) per_cu = 1;
     h->L.stagger_wgs = ncu * per_cu;
     // only launches of several rounds: one round has no later workgroups to keep the offsets
@@ -3193,6 +3372,16 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
       ALLOC(streams[k]->buf, n);
     }
   if (c.visited_penalty != 0.0) ALLOC(S.visited, n * (uint64_t)c.vis_words);
+  if (c.nt > kSmallTiles) {  // maps of > 64 tiles read their edge table from global memory
+    uint32_t* e = nullptr;
+    ALLOC(e, h->epk.size());
+    if (hipMemcpy(e, h->epk.data(), h->epk.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+      g_create_err = "edge table upload failed";
+      pgtg_destroy(h);
+      return PGTG_E_DEVICE;
+    }
+    S.epk = e;
+  }
   if (c.need_car) {
     ALLOC(S.car_w0, (uint64_t)c.car_slots * n);
     ALLOC(S.car_w1, (uint64_t)c.car_slots * n);
@@ -3232,14 +3421,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     memcpy(t.spawner, hs::kLaneSpawner, sizeof t.spawner);
     memcpy(t.lanes, hs::kLanes, sizeof t.lanes);
     memcpy(t.ind, c.ind_reward, sizeof t.ind);
-    for (int e = 0; e < c.n_edges; e++) {
-      int a = c.ea[e], b = c.eb[e], d = c.ed[e];
-      if (d == 0 || d == 3) {  // orient: a = north/west tile, d in {E (1), S (2)}
-        std::swap(a, b);
-        d = d == 0 ? 2 : 1;
-      }
-      t.epk[e] = (uint32_t)a | (uint32_t)b << 8 | (uint32_t)d << 16 | (uint32_t)c.erev[e] << 24;
-    }
+    if (c.n_edges <= kSmallEdges) memcpy(t.epk, h->epk.data(), h->epk.size() * sizeof(uint32_t));
     memcpy(t.bt, c.bt, sizeof t.bt);
     memcpy(t.bd, c.bd, sizeof t.bd);
     for (int k = 0; k < PGTG_MAX_CHANNELS; k++) t.chan[k] = (uint8_t)c.channels[k];
@@ -3330,15 +3512,14 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
     }
     HIPCHK(h, hipEventRecord(h->evpool[h->ev_used], h->stream));
   }
-  if (h->hcfg.need_car || h->hcfg.n_rules > 0)
-    hipLaunchKernelGGL(k_env<true>, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
-                       actions, mask, h->out, mode, h->L, h->tr_slot);
-  else if (mode == MODE_STEP && h->L.queue)
-    hipLaunchKernelGGL(k_envq, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
-                       actions, h->out, h->L);
-  else
-    hipLaunchKernelGGL(k_env<false>, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
-                       actions, mask, h->out, mode, h->L, h->tr_slot);
+  const void* fn = step_fn(h, mode);
+  void* args[] = {&h->dcfg, &h->dtab, &h->S, &actions, &mask, &h->out, &mode, &h->L, &h->tr_slot};
+  if (fn == (const void*)k_envq<false> || fn == (const void*)k_envq<true>) {
+    void* qargs[] = {&h->dcfg, &h->dtab, &h->S, &actions, &h->out, &h->L};
+    HIPCHK(h, hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(kBlock), qargs, h->lds, h->stream));
+  } else {
+    HIPCHK(h, hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(kBlock), args, h->lds, h->stream));
+  }
   HIPCHK(h, hipGetLastError());
   if (h->hcfg.need_car && mode != MODE_OBSERVE) {
     // initial traffic of the envs reset by this launch, then (windows other than the agent's tile)
@@ -3349,8 +3530,12 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
     if (!h->hcfg.obs_fast && h->hcfg.traffic_ch >= 0) {
       PgtgOutputs o{};
       o.obs = h->out.obs;  // only the observation: positions etc. are unchanged
-      hipLaunchKernelGGL(k_env<true>, dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab, h->S,
-                         nullptr, nullptr, o, (int)MODE_OBSERVE, h->L, h->tr_slot);
+      if (h->hcfg.nt > kSmallTiles)
+        hipLaunchKernelGGL((k_env<true, true>), dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab,
+                           h->S, nullptr, nullptr, o, (int)MODE_OBSERVE, h->L, h->tr_slot);
+      else
+        hipLaunchKernelGGL((k_env<true, false>), dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab,
+                           h->S, nullptr, nullptr, o, (int)MODE_OBSERVE, h->L, h->tr_slot);
       HIPCHK(h, hipGetLastError());
     }
     h->tr_slot ^= 1u;
@@ -3427,13 +3612,19 @@ int pgtg_get_env_state(pgtg_handle* h, uint64_t env, PgtgEnvState* st) {
   st->vx = (int16_t)(r.a.y & 0xffffu);
   st->vy = (int16_t)(r.a.y >> 16);
   st->phase = (int)(r.a.z & 0xffffu);
-  uint32_t fl = (r.a.z >> 16) & 0xffu;
+  uint32_t fl = (r.a.z >> 16) & 0xfu;
   st->terminated = (fl & kFlagTerminated) ? 1 : 0;
   st->flat_tire = (fl & kFlagFlatTire) ? 1 : 0;
-  st->path_len = (int)(r.a.z >> 24);
+  st->path_len = (int)(r.a.z >> 20);
   st->elapsed = (int)r.a.w;
   st->spawn_counter = r.b.y;
   st->used_subgoals = (uint64_t)r.b.z | ((uint64_t)r.b.w << 32);
+  if (h->hcfg.nt > kSmallTiles) {  // maps of > 64 tiles mark the plan words: report tiles 0..63
+    std::vector<uint16_t> p(h->hcfg.plan_stride);
+    HIPCHK(h, hipMemcpy(p.data(), h->S.plan + env * (uint64_t)h->hcfg.plan_stride, p.size() * 2, hipMemcpyDeviceToHost));
+    st->used_subgoals = 0;
+    for (int t = 0; t < 64; t++) st->used_subgoals |= (uint64_t)((p[t] & kPlanUsed) != 0) << t;
+  }
   st->seed = seed;
   st->error = -(int)e;
   if (h->hcfg.need_car) {
@@ -3789,9 +3980,9 @@ int pgtg_set_to_state(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_
   HIPCHK(h, hipMemcpy(&r, h->S.rec + env, sizeof r, hipMemcpyDeviceToHost));
   r.a.x = ((uint32_t)x & 0xffffu) | ((uint32_t)y << 16);
   r.a.y = ((uint32_t)vx & 0xffffu) | ((uint32_t)vy << 16);
-  uint32_t flags = (r.a.z >> 16) & 0xffu;
+  uint32_t flags = (r.a.z >> 16) & 0xfu;
   flags = flat_tire ? (flags | kFlagFlatTire) : (flags & ~kFlagFlatTire);
-  r.a.z = (r.a.z & 0xff00ffffu) | (flags << 16);
+  r.a.z = (r.a.z & 0xfff0ffffu) | (flags << 16);
   HIPCHK(h, hipMemcpy(h->S.rec + env, &r, sizeof r, hipMemcpyHostToDevice));
   if (c.need_car) {
     uint4 t;
@@ -3927,16 +4118,17 @@ int pgtg_window(const pgtg_handle* h) { return h ? h->hcfg.win : 0; }
 uint64_t pgtg_num_envs(const pgtg_handle* h) { return h ? h->n : 0; }
 const char* pgtg_step_kernel(const pgtg_handle* h) {
   if (!h) return "";
-  if (h->hcfg.need_car) return "pgtg::k_env<true> + pgtg::k_traffic";
-  if (h->hcfg.n_rules > 0) return "pgtg::k_env<true>";
-  return h->L.queue ? "pgtg::k_envq" : "pgtg::k_env<false>";
+  const bool big = h->hcfg.nt > kSmallTiles;
+  if (h->hcfg.need_car) return big ? "pgtg::k_env<true, true> + pgtg::k_traffic" : "pgtg::k_env<true, false> + pgtg::k_traffic";
+  if (h->hcfg.n_rules > 0) return big ? "pgtg::k_env<true, true>" : "pgtg::k_env<true, false>";
+  if (h->L.queue) return big ? "pgtg::k_envq<true>" : "pgtg::k_envq<false>";
+  return big ? "pgtg::k_env<false, true>" : "pgtg::k_env<false, false>";
 }
 
 int pgtg_occupancy(const pgtg_handle* h, int32_t* step_blocks_per_cu) {
   if (!h) return PGTG_E_INVALID;
   int nb = 0;
-  const bool tr = h->hcfg.need_car || h->hcfg.n_rules > 0;  // the kernel launch() picks
-  const void* fn = tr ? (const void*)k_env<true> : (h->L.queue ? (const void*)k_envq : (const void*)k_env<false>);
+  const void* fn = step_fn(h, MODE_STEP);  // the kernel launch() picks
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kBlock, h->lds) != hipSuccess) return PGTG_E_DEVICE;
   if (step_blocks_per_cu) *step_blocks_per_cu = nb;
   return PGTG_OK;

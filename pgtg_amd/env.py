@@ -13,7 +13,8 @@ with `obs = {"position": int64[2], "velocity": int64[2], "map": {feature: int64[
 effect") like the reference (:1109-1110).  Differences, by design:
   * `obs["velocity"]` is a copy; the reference returns an alias of its internal state (:1462);
   * `reward` is always a Python float (the reference returns int 0 when nothing was scored);
-  * rendering (pgtg/graphic.py) is out of scope: `render_mode` must be None.
+  * rendering (pgtg/graphic.py) is out of scope: `render_mode` is validated and kept like the
+    reference's (environment.py:790), but `render()` draws nothing and returns None.
 """
 from __future__ import annotations
 
@@ -154,11 +155,8 @@ class PGTGEnv:
     metadata = {"render_modes": []}
 
     def __init__(self, map_path: str | None = None, *, device: int | None = None, **kwargs: Any):
-        render_mode = kwargs.pop("render_mode", None)
-        if render_mode is not None:
-            raise Exception(f"render mode {render_mode!r} is not supported by this build (pgtg/graphic.py is out of scope)")
-        self.render_mode = None
-        self.spec = _cfg.make_spec(map_path, **kwargs)
+        self.spec = _cfg.make_spec(map_path, **kwargs)  # validates render_mode (environment.py:790)
+        self.render_mode = self.spec.render_mode
         self.map_path = map_path
         # room for cars appended by hand (env.cars.append(Car(...)), as the reference tests do)
         self._vec = PGTGVecEnv(1, spec=self.spec, device=device, autoreset=False, min_car_capacity=64)
@@ -232,6 +230,7 @@ class PGTGEnv:
         _cfg.save_map_plan(self._vec.map_plan(0), path)
 
     def render(self):
+        """Frames (pgtg/graphic.py) are out of scope for this build: nothing is drawn."""
         return None
 
     # -- state ----------------------------------------------------------------------------------

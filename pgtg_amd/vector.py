@@ -262,9 +262,9 @@ class PGTGVecEnv:
 
     def map_plan(self, i: int) -> dict:
         w, h = C.c_int32(), C.c_int32()
-        ex = (C.c_uint8 * 64)()
-        ot = (C.c_int8 * 64)()
-        om = (C.c_int8 * 64)()
+        ex = (C.c_uint8 * _abi.MAX_TILES)()
+        ot = (C.c_int8 * _abi.MAX_TILES)()
+        om = (C.c_int8 * _abi.MAX_TILES)()
         s3 = (C.c_int32 * 3)()
         g3 = (C.c_int32 * 3)()
         _check(self._lib.pgtg_get_map_plan(self._h, i, C.byref(w), C.byref(h), ex, ot, om, s3, g3), self._h)

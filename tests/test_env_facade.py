@@ -56,7 +56,9 @@ def test_facade_needs_the_device():
         PGTGEnv(random_map_width=3, random_map_height=3)
 
 
-def test_render_mode_rejected_before_device_use():
+def test_unknown_render_mode_rejected_before_device_use():
+    """environment.py:790 accepts None/human/rgb_array/pil_image and raises for anything else; this
+    happens in the config, before any device use."""
     from pgtg_amd.env import PGTGEnv
-    with pytest.raises(Exception, match="render mode"):
-        PGTGEnv(render_mode="human")
+    with pytest.raises(Exception, match="render_mode"):
+        PGTGEnv(render_mode="svg")

@@ -67,6 +67,20 @@ CONFIGS = {
     "tiny_1x1": (dict(random_map_width=1, random_map_height=1, traffic_density=0.5), None, 8, 30, "uniform"),
     "strip_2x1_full": (dict(random_map_width=2, random_map_height=1, random_map_percentage_of_connections=1.0),
                        None, 8, 30, "uniform"),
+    # maps of > 64 tiles (the 256-bit generator path): the reference's own integration-test env
+    # (tests/test_integration.py:25-42, 9x9), a 10x10 with obstacles and penalties, a 16x16 with traffic
+    "s9_integration": (dict(random_map_width=9, random_map_height=9, random_map_percentage_of_connections=0.9,
+                            random_map_obstacle_probability=0.8, random_map_broken_road_probability_weight=2,
+                            random_map_ice_probability_weight=4, random_map_sand_probability_weight=8,
+                            render_mode="pil_image", final_goal_bonus=100, standing_still_penalty=5,
+                            ice_probability=0.5, street_damage_probability=0.2, traffic_density=0.02,
+                            ignore_traffic_collisions=True), None, 8, 40, "uniform"),
+    "s10_obstacles": (dict(random_map_width=10, random_map_height=10, random_map_obstacle_probability=0.5,
+                           use_next_subgoal_direction=True, already_visited_position_penalty=1,
+                           separate_reward_cost=True), None, 6, 50, "cautious"),
+    "s16_traffic": (dict(random_map_width=16, random_map_height=16, random_map_percentage_of_connections=0.7,
+                         traffic_density=0.1, use_sliding_observation_window=True,
+                         sliding_observation_window_size=6), None, 3, 30, "cautious"),
     "fixed_1x1_traffic": (dict(traffic_density=1, ignore_traffic_collisions=True), "1x1_map", 4, 40, "still"),
     "fixed_crossing": (dict(traffic_density=0.5), "1x1_crossing_map", 4, 40, "cautious"),
     "fixed_4x1": (dict(sum_subgoals_reward=444), "4x1_map.json", 4, 40, "cautious"),
