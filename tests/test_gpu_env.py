@@ -238,16 +238,16 @@ def test_zero_traffic_rule_on_a_handle_without_traffic():
     cfg.add_rule(with_rule, rule)
     vec = PGTGVecEnv(48, spec=copy.deepcopy(base), device=0)
     try:
-        assert vec.step_kernel() == "pgtg::k_envq"
+        assert vec.step_kernel() == "pgtg::k_envq<false>"
         vec.reset(seed=70)
         vec.add_traffic_rule(rule)
-        assert vec.step_kernel() == "pgtg::k_env<true>"
+        assert vec.step_kernel() == "pgtg::k_env<true, false>"
         rng = np.random.default_rng(6)
         fired = _vec_vs_oracle(vec, with_rule, 48, 30, 70, rng, "rule")
         assert fired > 0
         # back without the rule: the state carries on; compare from a fresh seeded reset
         assert vec.remove_traffic_rule("brake_on_crossings")
-        assert vec.step_kernel() == "pgtg::k_envq"
+        assert vec.step_kernel() == "pgtg::k_envq<false>"
         vec.reset(seed=900)
         _vec_vs_oracle(vec, base, 48, 20, 900, rng, "no rule")
     finally:

@@ -13,6 +13,7 @@
 #   profile:<wl,..>  tools/gpu_profile.sh (rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes)
 #   stamps:<wl,..>   per-phase cycle stamps (PGTG_STAMPS build, tools/stamps.py)
 #   ab:<wl>:<lib>    interleaved bench lines of the in-tree library and <lib> (tools/ab_multi.sh, 3 reps)
+#   libtests:<lib>:<expr>  pytest -m gpu -k <expr> against another build of the library (PGTG_LIB)
 set -o pipefail
 TAG=$1
 shift
@@ -55,6 +56,10 @@ for S in "$@"; do
       python -c "from pgtg_amd.build import build; build(variant='stamps')" || exit 1
       timeout -k 10 300 python tools/stamps.py ${S#stamps:} > $O/stamps.log 2>&1 || { tail -20 $O/stamps.log; exit 1; }
       cat $O/stamps.log ;;
+    libtests:*)
+      R=${S#libtests:}; L=${R%%:*}; K=${R#*:}
+      PGTG_LIB=$PWD/$L timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -k "$K" > $O/pytest_lib.log 2>&1
+      rc=$?; tail -3 $O/pytest_lib.log; [ $rc = 0 ] || exit 1 ;;
     ab:*)
       R=${S#ab:}; W=${R%%:*}; L=${R#*:}
       timeout -k 10 900 bash tools/ab_multi.sh $W 3 new $L > $O/ab_$W.log 2>&1 || { tail -20 $O/ab_$W.log; exit 1; }
