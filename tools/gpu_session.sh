@@ -14,6 +14,7 @@
 #   stamps:<wl,..>   per-phase cycle stamps (PGTG_STAMPS build, tools/stamps.py)
 #   ab:<wl>:<lib>    interleaved bench lines of the in-tree library and <lib> (tools/ab_multi.sh, 3 reps)
 #   libtests:<lib>:<expr>  pytest -m gpu -k <expr> against another build of the library (PGTG_LIB)
+#   pmc:<wl>:<lib|new>     FETCH_SIZE / WRITE_SIZE passes of one workload with a given library
 set -o pipefail
 TAG=$1
 shift
@@ -60,6 +61,15 @@ for S in "$@"; do
       R=${S#libtests:}; L=${R%%:*}; K=${R#*:}
       PGTG_LIB=$PWD/$L timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -k "$K" > $O/pytest_lib.log 2>&1
       rc=$?; tail -3 $O/pytest_lib.log; [ $rc = 0 ] || exit 1 ;;
+    pmc:*)
+      R=${S#pmc:}; W=${R%%:*}; L=${R#*:}; N=$(basename $L .so)
+      D=$O/pmc_${W}_$N
+      if [ $L = new ]; then unset PGTG_LIB; else export PGTG_LIB=$PWD/$L; fi
+      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $D/fetch -o run --output-format csv -- python bench.py --workload $W --steps 40 --warmup 10 --no-cpu-baseline > /dev/null 2>$D.err || { tail $D.err; exit 1; }
+      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $D/write -o run --output-format csv -- python bench.py --workload $W --steps 40 --warmup 10 --no-cpu-baseline > /dev/null 2>>$D.err || { tail $D.err; exit 1; }
+      unset PGTG_LIB
+      python tools/pmc.py $W $D/fetch $D/write $N > $D.json || exit 1
+      python -c "import json; d=json.load(open('$D.json')); print('$W $N', {k: round((v['read_bytes']+v['write_bytes'])/1e6,1) for k,v in d.items() if isinstance(v,dict)}, round(d['hbm_bytes_per_launch']/1e6,1), 'MB/launch')" ;;
     ab:*)
       R=${S#ab:}; W=${R%%:*}; L=${R#*:}
       timeout -k 10 900 bash tools/ab_multi.sh $W 3 new $L > $O/ab_$W.log 2>&1 || { tail -20 $O/ab_$W.log; exit 1; }
