@@ -395,8 +395,15 @@ __device__ __forceinline__ bool mask_any(const Bits<NW>& m) {
   for (int q = 0; q < NW; q++) o |= m.w[q];
   return o != 0ull;
 }
-template <typename M>
-__device__ __forceinline__ bool mask_eq(const M& a, const M& b) { return !mask_any((a & ~b) | (b & ~a)); }
+__device__ __forceinline__ bool mask_eq(uint32_t a, uint32_t b) { return a == b; }
+__device__ __forceinline__ bool mask_eq(uint64_t a, uint64_t b) { return a == b; }
+template <int NW>
+__device__ __forceinline__ bool mask_eq(const Bits<NW>& a, const Bits<NW>& b) {
+  uint64_t d = 0;
+#pragma unroll
+  for (int q = 0; q < NW; q++) d |= a.w[q] ^ b.w[q];
+  return d == 0ull;
+}
 __device__ __forceinline__ bool mask_get(uint32_t m, int t) { return (m >> t) & 1u; }
 __device__ __forceinline__ bool mask_get(uint64_t m, int t) { return (m >> t) & 1ull; }
 template <int NW>
@@ -778,16 +785,34 @@ __device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, int
   }
   STAMP(25);
   int v = s, len = 1;
-  while (v != g) {  // the walk marks the direction to the next tile on every path tile but the goal's
-    uint32_t d;
-    int nv;
-    if (mask_get(cN, v)) { d = 1u; nv = v - w; }
-    else if (mask_get(cE, v)) { d = 2u; nv = v + 1; }
-    else if (mask_get(cS, v)) { d = 3u; nv = v + w; }
-    else { d = 4u; nv = v - 1; }
-    plan[v] = (uint16_t)((plan[v] & ~(7u << 11)) | d << 11);
-    v = nv;
-    len++;
+  if constexpr (sizeof(M) <= 8) {  // <= 64 tiles: the walk in registers, then the plan marks
+    M pN = 0, pE = 0, pS = 0, pW = 0;
+    while (v != g) {
+      const M b = (M)1 << v;
+      if (cN & b) { pN |= b; v -= w; }
+      else if (cE & b) { pE |= b; v += 1; }
+      else if (cS & b) { pS |= b; v += w; }
+      else { pW |= b; v -= 1; }
+      len++;
+    }
+    for (M m = pN | pE | pS | pW; m; m &= m - 1) {
+      const int t = __builtin_ctzll((uint64_t)m);
+      const M b = (M)1 << t;
+      const uint32_t d = (pN & b) ? 1u : (pE & b) ? 2u : (pS & b) ? 3u : 4u;
+      plan[t] = (uint16_t)((plan[t] & ~(7u << 11)) | d << 11);
+    }
+  } else {  // larger maps: each path tile marked as the walk passes it
+    while (v != g) {
+      uint32_t d;
+      int nv;
+      if (mask_get(cN, v)) { d = 1u; nv = v - w; }
+      else if (mask_get(cE, v)) { d = 2u; nv = v + 1; }
+      else if (mask_get(cS, v)) { d = 3u; nv = v + w; }
+      else { d = 4u; nv = v - 1; }
+      plan[v] = (uint16_t)((plan[v] & ~(7u << 11)) | d << 11);
+      v = nv;
+      len++;
+    }
   }
   return len;
 }
