@@ -51,11 +51,10 @@ struct EnvRec {
 struct DevCfg {
   int32_t tw, th, nt, W, H;
   int32_t fixed_map;
-  uint16_t fixed_plan[kMaxTiles];
   uint32_t fixed_sg;
   int32_t start_mode, goal_mode, sx, sy, sdir, gx, gy, gdir, min_distance;
   int32_t n_edges, keep;
-  uint64_t h0[4][4];  // full-grid exit masks (N, E, S, W) before removals, 4 x 64 tiles
+  uint64_t h0[4][4];  // full-grid exit masks before removals: h0[64-tile word][N, E, S, W]
   int32_t n_border, n_border_add;
   uint8_t bt[kMaxBorder], bd[kMaxBorder];
   double obstacle_probability;
@@ -64,7 +63,6 @@ struct DevCfg {
   int32_t phase_total, phase_g, phase_gy;
   int32_t ignore_collisions, separate_cost, autoreset, max_steps;
   double crash_penalty, final_goal_bonus, tl_penalty, still_penalty, visited_penalty;
-  double ind_reward[kMaxTiles + 1];
   int32_t n_channels, win, sliding, ss, next_subgoal, generic_channels;
   int32_t channels[PGTG_MAX_CHANNELS];
   int32_t need_car, need_ice, need_broken, need_sand;
@@ -95,6 +93,9 @@ struct DevCfg {
   int32_t obs_bytes;            // n_channels * win * win
   int32_t qrec_dw;              // map-queue entry words (plan_stride / 2 + 4)
   int32_t mask_words;           // ceil(win*win/32)
+  // per-tile arrays of maps up to 256 tiles, kept behind the fields every launch reads
+  uint16_t fixed_plan[kMaxTiles];
+  double ind_reward[kMaxTiles + 1];
 };
 
 // Lane-indexed constant tables, copied once per workgroup into LDS (sT in pgtg_env.hip): the

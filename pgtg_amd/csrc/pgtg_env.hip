@@ -448,13 +448,13 @@ __device__ __forceinline__ int mask_ctz(const Bits<NW>& m) {
 // the full-grid exit mask of direction d (DevCfg::h0) as an M
 template <typename M>
 __device__ __forceinline__ M mask_h0(const DevCfg& c, int d) {
-  return (M)c.h0[d][0];
+  return (M)c.h0[0][d];
 }
 template <>
 __device__ __forceinline__ Bits<4> mask_h0<Bits<4>>(const DevCfg& c, int d) {
   Bits<4> r;
 #pragma unroll
-  for (int q = 0; q < 4; q++) r.w[q] = c.h0[d][q];
+  for (int q = 0; q < 4; q++) r.w[q] = c.h0[q][d];
   return r;
 }
 
@@ -701,12 +701,12 @@ __device__ __forceinline__ void generate_map(const DevCfg& c, const uint32_t* __
   } else {
     uint64_t hN, hE, hS, hW;
     if (c.nt <= 32) {
-      uint32_t n = (uint32_t)c.h0[0][0], e = (uint32_t)c.h0[1][0], so = (uint32_t)c.h0[2][0], we = (uint32_t)c.h0[3][0];
+      uint32_t n = (uint32_t)c.h0[0][0], e = (uint32_t)c.h0[0][1], so = (uint32_t)c.h0[0][2], we = (uint32_t)c.h0[0][3];
       if (c.n_edges <= 64) remove_edges<uint32_t, 1>(c, epk, r, st_t, gl_t, n, e, so, we);
       else remove_edges<uint32_t, 2>(c, epk, r, st_t, gl_t, n, e, so, we);
       hN = n; hE = e; hS = so; hW = we;
     } else {
-      hN = c.h0[0][0]; hE = c.h0[1][0]; hS = c.h0[2][0]; hW = c.h0[3][0];
+      hN = c.h0[0][0]; hE = c.h0[0][1]; hS = c.h0[0][2]; hW = c.h0[0][3];
       remove_edges<uint64_t, 4>(c, epk, r, st_t, gl_t, hN, hE, hS, hW);
     }
     for (int t = 0; t < c.nt; t++)
@@ -3050,7 +3050,7 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
     if (n > kMaxEdges) return fail(h, PGTG_E_UNSUPPORTED, "too many map edges");
     c.n_edges = n;
     memset(c.h0, 0, sizeof c.h0);
-    for (int e = 0; e < n; e++) c.h0[ed[e]][ea[e] >> 6] |= 1ull << (ea[e] & 63);
+    for (int e = 0; e < n; e++) c.h0[ea[e] >> 6][ed[e]] |= 1ull << (ea[e] & 63);
     // the edge table (Tables::epk / DevState::epk): a = north/west tile, horizontal flag, reverse edge
     std::vector<int> pos(c.nt * 4, -1);  // (tile, direction) -> list index
     for (int e = 0; e < n; e++) pos[ea[e] * 4 + ed[e]] = e;
