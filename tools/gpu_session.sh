@@ -12,6 +12,7 @@
 #                    131 072 envs) beside the 1 048 576-env line
 #   profile:<wl,..>  tools/gpu_profile.sh (rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes)
 #   stamps:<wl,..>   per-phase cycle stamps (PGTG_STAMPS build, tools/stamps.py)
+#   stampslib:<lib>:<wl>  the same with a prebuilt stamps library
 #   ab:<wl>:<lib>    interleaved bench lines of the in-tree library and <lib> (tools/ab_multi.sh, 3 reps)
 #   libtests:<lib>:<expr>  pytest -m gpu -k <expr> against another build of the library (PGTG_LIB)
 #   pmc:<wl>:<lib|new>     FETCH_SIZE / WRITE_SIZE passes of one workload with a given library
@@ -57,6 +58,10 @@ for S in "$@"; do
       python -c "from pgtg_amd.build import build; build(variant='stamps')" || exit 1
       timeout -k 10 300 python tools/stamps.py ${S#stamps:} > $O/stamps.log 2>&1 || { tail -20 $O/stamps.log; exit 1; }
       cat $O/stamps.log ;;
+    stampslib:*)
+      R=${S#stampslib:}; L=${R%%:*}; W=${R#*:}
+      PGTG_STAMPS_LIB=$PWD/$L timeout -k 10 300 python tools/stamps.py $W > $O/stamps_$(basename $L .so).log 2>&1 || { tail -20 $O/stamps_$(basename $L .so).log; exit 1; }
+      cat $O/stamps_$(basename $L .so).log ;;
     libtests:*)
       R=${S#libtests:}; L=${R%%:*}; K=${R#*:}
       PGTG_LIB=$PWD/$L timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -k "$K" > $O/pytest_lib.log 2>&1
