@@ -106,6 +106,34 @@ def load_traffic(workload: str, n_envs: int):
     return d.get("hbm_bytes_per_launch"), p
 
 
+# Issue roofline: one instruction per SIMD per cycle at the 2 400 MHz engine clock (MI355X_MICROARCH.md:
+# 256 CUs x 4 SIMDs), and the VALU's own ceiling (a wave64 VALU instruction issues over 2 cycles)
+PEAK_ISSUE = 256 * 4 * 2.4e9
+PEAK_VALU = PEAK_ISSUE / 2
+
+
+def load_issue(workload: str, n_envs: int, avg_kernel_s: float):
+    """Issue roofline from the committed SQ counters of this workload (profiles/sq_<workload>.json,
+    tools/sq_json.py): executed VALU + SALU wave-instructions of the step's kernels per launch over the
+    average launch duration measured in this run."""
+    p = os.path.join("profiles", f"sq_{workload}.json")
+    try:
+        with open(os.path.join(ROOT, p)) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("envs") != n_envs or avg_kernel_s <= 0:
+        return None
+    valu = sum(k.get("SQ_INSTS_VALU", 0.0) for k in d["kernels"].values())
+    salu = sum(k.get("SQ_INSTS_SALU", 0.0) for k in d["kernels"].values())
+    insts = valu + salu
+    return {"bound": "issue", "unit": "wave-instructions/s", "achieved": insts / avg_kernel_s, "peak": PEAK_ISSUE,
+            "frac": insts / avg_kernel_s / PEAK_ISSUE, "valu_frac": valu / avg_kernel_s / PEAK_VALU,
+            "valu_per_launch": valu, "salu_per_launch": salu, "insts_per_env_step": insts / n_envs,
+            "peak_model": "256 CU x 4 SIMD x 2.4 GHz, one instruction per SIMD-cycle (VALU: one per 2)",
+            "kernels": sorted(d["kernels"]), "source": p}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -246,6 +274,9 @@ def main():
                          "envs_per_workgroup": env.launch_info()[0], "lds_bytes": env.launch_info()[1],
                          "workgroups_per_cu": env.occupancy()},
         }
+        issue = load_issue(args.workload, n_local, avg_kernel_s)
+        if issue is not None:
+            rec["roofline_issue"] = issue
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)
         print(json.dumps(rec), flush=True)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PGTG_ABI_VERSION 4
+#define PGTG_ABI_VERSION 5
 
 /* status codes (Python facade maps them to the reference's exception types) */
 #define PGTG_OK 0
@@ -115,6 +115,8 @@ typedef struct {
   int32_t tune_obs_sub;                /* envs per observation sub-batch */
   int32_t tune_kt_grid, tune_kt_cap, tune_kt_wpc; /* k_traffic grid, envs per wave, workgroups per CU */
   int32_t tune_car_slots;              /* car slots per env (>= 3 x capacity + 4; tests of the bound) */
+  int32_t tune_kt_serial;              /* 1: initial traffic's per-car draws on one lane per env (the
+                                          rejection fallback of the lane-parallel path; tests) */
 } PgtgConfig;
 
 /* Output buffers (device pointers, caller-owned, contiguous).  NULL = not produced. */

@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 # PGTG_LIB selects another build of the same library (test variants, pgtg_amd/build.py VARIANTS)
 LIB_PATH = os.environ.get("PGTG_LIB") or os.path.join(PKG, "libpgtg_hip.so")
 
-PGTG_ABI_VERSION = 4
+PGTG_ABI_VERSION = 5
 MAX_TILES = 256
 MAX_CHANNELS = 48
 MAX_RULES = 8
@@ -66,6 +66,7 @@ class PgtgConfig(C.Structure):
         ("autoreset", C.c_int32), ("max_episode_steps", C.c_int32), ("min_car_capacity", C.c_int32),
         ("tune_envs_per_block", C.c_int32), ("tune_obs_sub", C.c_int32), ("tune_kt_grid", C.c_int32),
         ("tune_kt_cap", C.c_int32), ("tune_kt_wpc", C.c_int32), ("tune_car_slots", C.c_int32),
+        ("tune_kt_serial", C.c_int32),
     ]
 
 
@@ -160,7 +161,7 @@ def fill_rules(dst, rules) -> int:
     return len(rules)
 
 
-TUNE_KEYS = ("envs_per_block", "obs_sub", "kt_grid", "kt_cap", "kt_wpc", "car_slots")
+TUNE_KEYS = ("envs_per_block", "obs_sub", "kt_grid", "kt_cap", "kt_wpc", "car_slots", "kt_serial")
 
 
 def config_struct(spec: "cfgmod.EnvSpec", autoreset: bool, max_episode_steps: int | None,

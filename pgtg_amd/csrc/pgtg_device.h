@@ -69,6 +69,8 @@ struct DevCfg {
   double density;
   uint64_t profile_t[5];  // profile CDF as 53-bit thresholds: random() < cdf[j]  <=>  (next64 >> 11) < t[j]
   int32_t car_cap;      // cars an env can hold (initial traffic <= this; pgtg_add_car / set_to_state limit)
+  int32_t kt_serial;    // initial traffic's per-car draws on one lane per env (PgtgConfig.tune_kt_serial)
+  int32_t kt_jump_bits; // bound of the jump lengths of the lane-parallel per-car draws (< 2^bits outputs)
   int32_t car_slots;    // car slots per env (>= 2 * car_cap: empty slots + a tick of respawns)
   int32_t max_spawners; // spawner list capacity per env (nt * 5)
   // DRIVER_BEHAVIORS (pgtg/environment.py:64-109) in DriverProfile order, thresholds precomputed
@@ -78,6 +80,7 @@ struct DevCfg {
   int32_t traf_bytes;      // k_env per-lane LDS traffic region: occupancy counters, spawner cache
   int32_t sp_cache_off;    // byte offset of the spawner cache (kSpCache entries) in it
   int32_t rs_bytes;        // k_traffic per-lane reset scratch: Floyd output [0, 2*cap), seen set, column prefix
+  int32_t rs_jj_off;       // the shuffle's draws (u16 x cap)
   int32_t rs_seen_off;
   int32_t rs_pre_off;
   int32_t rs_cm_off;        // per-column masks of spawnable rows (u32 pairs; maps of <= 7 tile rows, else 0)
@@ -334,6 +337,51 @@ __device__ __forceinline__ uint64_t ahead_draw(PcgAhead& a, bool is_int, uint32_
 __device__ __forceinline__ uint32_t ahead_int(PcgAhead& a, uint32_t n) {
   if (n <= 1u) return 0u;
   return (uint32_t)ahead_draw(a, true, n);
+}
+
+// ------------------------------------------------------------------------------------------------
+// PCG64 jump-ahead.  s_{n+d} = M^d s_n + (1 + M + ... + M^(d-1)) inc, so a jump of d outputs
+// composes the jumps of d's set bits: kPcgJump[b] = {M^(2^b), G(2^b)} (hi, lo words), G(2d) = G(d)
+// (1 + M^d), M^(2d) = (M^d)^2.  Lanes that evaluate disjoint stretches of one stream start there.
+// ------------------------------------------------------------------------------------------------
+constexpr int kJumpBits = 16;  // jumps of < 65 536 outputs
+struct JumpTab {
+  uint64_t v[kJumpBits][4];  // M^(2^b) hi, lo, G(2^b) hi, lo
+};
+constexpr JumpTab make_jump_tab() {
+  JumpTab t{};
+  unsigned __int128 m = ((unsigned __int128)0x2360ED051FC65DA4ull << 64) | 0x4385DF649FCCF645ull, gsum = 1;
+  for (int b = 0; b < kJumpBits; b++) {
+    t.v[b][0] = (uint64_t)(m >> 64);
+    t.v[b][1] = (uint64_t)m;
+    t.v[b][2] = (uint64_t)(gsum >> 64);
+    t.v[b][3] = (uint64_t)gsum;
+    gsum = gsum * (m + 1);
+    m = m * m;
+  }
+  return t;
+}
+__constant__ constexpr JumpTab kPcgJump = make_jump_tab();
+
+// (ahi:alo) * (bhi:blo) mod 2^128
+__device__ __forceinline__ void mul128(uint64_t ahi, uint64_t alo, uint64_t bhi, uint64_t blo, uint64_t& rhi, uint64_t& rlo) {
+  rlo = alo * blo;
+  rhi = __umul64hi(alo, blo) + alo * bhi + ahi * blo;
+}
+// advance g by d outputs (d < 2^nbits; nbits wave-uniform bounds the loop); the 32-bit buffer is
+// left as it is
+__device__ __forceinline__ void pcg_advance(Pcg& g, uint32_t d, int nbits) {
+  for (int b = 0; b < nbits; b++) {
+    if ((d >> b) & 1u) {
+      const uint64_t mh = kPcgJump.v[b][0], ml = kPcgJump.v[b][1], gh = kPcgJump.v[b][2], gl = kPcgJump.v[b][3];
+      uint64_t sh, sl, ch, cl;
+      mul128(g.shi, g.slo, mh, ml, sh, sl);
+      mul128(g.ihi, g.ilo, gh, gl, ch, cl);
+      const uint64_t lo = sl + cl;
+      g.shi = sh + ch + (lo < sl ? 1ull : 0ull);
+      g.slo = lo;
+    }
+  }
 }
 
 // choice(k, p=p) with the host-normalised CDF (cumsum(p)/cumsum[-1]) as 53-bit thresholds:

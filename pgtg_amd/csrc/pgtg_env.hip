@@ -67,11 +67,14 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // One env's tile plan (plan_stride u16 words in HBM, a multiple of 8) into its LDS row of pdw words,
-// in blocks of 8 x 16 bytes (one block for maps of <= 64 tiles), each block's loads first.
+// in blocks of 8 x 16 bytes (BIG: maps of > 64 tiles; smaller maps are one block, straight-line code:
+// a runtime block loop made the compiler wait for every load before the first LDS store), each
+// block's loads first.
+template <bool BIG>
 __device__ __forceinline__ void stage_plan(const uint16_t* __restrict__ plan, int plan_stride, uint32_t* dst, int pdw) {
   const uint4* src = reinterpret_cast<const uint4*>(plan);
   const int nq = plan_stride / 8;
-  for (int k0 = 0; k0 < nq; k0 += 8) {
+  for (int k0 = 0; k0 < (BIG ? nq : 1); k0 += 8) {
     uint4 q[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) q[k] = src[k0 + k < nq ? k0 + k : k0];  // unconditional: registers, not scratch
@@ -284,6 +287,19 @@ __device__ __forceinline__ void occ_inc(uint8_t* o, int s, bool& sat) {
 __device__ __forceinline__ int occ_at(const DevCfg& c, const Plan& pl, const uint8_t* occ, int x, int y) {
   int s = lane_slot(c, pl, x, y);
   return s < 0 ? 0 : occ_get(occ, s);
+}
+// k-th (0-based) set bit of a 32-bit word, branch-free (popcount halving); -1 if there is none
+__device__ __forceinline__ int select32(uint32_t x, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int sh = 16; sh >= 1; sh >>= 1) {
+    const int c = __popc(x & ((1u << sh) - 1u));
+    const bool up = k >= c;
+    k -= up ? c : 0;
+    x = up ? x >> sh : x;
+    pos += up ? sh : 0;
+  }
+  return (x & 1u) && k == 0 ? pos : -1;
 }
 __device__ __forceinline__ int kth_bit(uint32_t m, int k) {
   for (int j = 0; j < k; j++) m &= m - 1u;
@@ -841,6 +857,280 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
+// One car of the initial traffic (pgtg/environment.py:840-879): square code -> lanes of the square
+constexpr int kCarChunk = 4;  // cars whose lookups cars_group issues together
+struct CarSquare {
+  int x, y, tile, sq;
+  uint32_t rl, nr;  // route lanes (kLanes bits 0..27) and their count
+};
+__device__ __forceinline__ CarSquare car_square(const DevCfg& c, const Plan& pl, uint32_t code) {
+  CarSquare q;
+  q.x = (int)(code & 255u);
+  q.y = (int)(code >> 8);
+  const int tx = (int)((uint32_t)q.x / (uint32_t)kTile), ty = (int)((uint32_t)q.y / (uint32_t)kTile);
+  q.tile = ty * c.tw + tx;
+  q.sq = (q.x - tx * kTile) * 9 + (q.y - ty * kTile);
+  q.rl = sT.lanes[plan_exits(pl[q.tile])][q.sq] & 0x0fffffffu;
+  q.nr = __popc(q.rl);
+  return q;
+}
+// the squares of cars m .. m+U-1 (indices clamped to mend-1, so every read is unconditional: a
+// level's LDS reads go out together instead of one dependent chain per car)
+template <int U>
+__device__ __forceinline__ void car_squares(const DevCfg& c, const Plan& pl, const uint16_t* out, int m, int mend,
+                                            CarSquare* q) {
+  uint32_t code[U], p[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) code[u] = out[min(m + u, mend - 1)];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    q[u].x = (int)(code[u] & 255u);
+    q[u].y = (int)(code[u] >> 8);
+    const int tx = (int)((uint32_t)q[u].x / (uint32_t)kTile), ty = (int)((uint32_t)q[u].y / (uint32_t)kTile);
+    q[u].tile = ty * c.tw + tx;
+    q[u].sq = (q[u].x - tx * kTile) * 9 + (q[u].y - ty * kTile);
+    p[u] = pl[q[u].tile];
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    q[u].rl = sT.lanes[plan_exits(p[u])][q[u].sq] & 0x0fffffffu;
+    q[u].nr = __popc(q[u].rl);
+  }
+}
+__device__ __forceinline__ void store_new_car(const CarSlots& cs, uint64_t a, const CarSquare& q, int route, int prof, int m) {
+  cs.w0[a] = (uint32_t)q.x | (uint32_t)q.y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
+  cs.w1[a] = 0u;
+  cs.id[a] = (uint32_t)m;
+}
+
+// The per-car draws on one lane, in id order: random() -> profile, then choice(routes) when the
+// square has more than one route (numpy draws nothing for one).  `cr` enters as the stream after the
+// shuffle and leaves after the last car.
+__device__ __forceinline__ int cars_serial(const DevCfg& c, const CarSlots& cs, const Plan& pl, const uint16_t* out, int k,
+                                        int at, uint32_t* CR, Pcg& cr) {
+  const ProfileCdf pcdf = pin_profile_cdf(c);
+  PcgAhead ca = ahead_init(cr);
+  CR[0] = CR[1] = CR[2] = 0u;
+  uint64_t a_m = cs.at(0);
+  for (int m = 0; m < k; m++) {
+    const CarSquare q = car_square(c, pl, out[m]);
+    if (q.tile == at) CR[q.sq >> 5] |= 1u << (q.sq & 31);
+    if (q.nr == 0) return PGTG_E_MAP;  // "a car was spawned on a field where no car lane was found"
+    const uint64_t u = ahead_draw(ca, false, 0u);
+    const int prof = profile_of(pcdf, u);
+    const uint32_t rk = q.nr > 1u ? (uint32_t)ahead_draw(ca, true, q.nr) : 0u;
+    store_new_car(cs, a_m, q, sT.lane_route[kth_bit(q.rl, (int)rk)], prof, m);
+    a_m += cs.n;
+  }
+  cr = ca.g;
+  return 0;
+}
+
+// The same draws split over the g lanes of the env's group, lane `sub` taking cars [k sub/g,
+// k (sub+1)/g).  Each car consumes one 64-bit output for its profile double and, when it has more
+// than one route, one 32-bit half (numpy's next_uint32: the low half of a fresh output, whose high
+// half is buffered for the next such draw; doubles do not touch the buffer).  So the stream position
+// of every car follows from the counts of multi-route cars before it: the lanes count theirs, take
+// prefix sums over the group, jump their copy of the stream there (pcg_advance) and draw their cars
+// like the serial loop.  Lemire rejections (left < 2^32 mod n, probability < n / 2^32 per draw) would
+// shift every later position: a group that meets one redoes the cars on one lane (cars_serial).
+// Returns lane 0's result; on return every lane holds the stream after the last car in `cr` and
+// lane 0 the group's agent-tile car squares in CR.
+__device__ __forceinline__ int cars_group(const DevCfg& c, const CarSlots& cs, const Plan& pl, const uint16_t* out,
+                                          int k, int at, uint32_t* CR, Pcg& cr, int sub, int g) {
+  const int q0 = (int)(threadIdx.x & 63u) - sub;  // the group's first lane
+  // lane 0's post-shuffle stream to the group
+  {
+    const uint32_t a0 = __shfl((uint32_t)cr.shi, q0), a1 = __shfl((uint32_t)(cr.shi >> 32), q0);
+    const uint32_t a2 = __shfl((uint32_t)cr.slo, q0), a3 = __shfl((uint32_t)(cr.slo >> 32), q0);
+    const uint32_t a4 = __shfl(cr.buf, q0), a5 = __shfl(cr.has, q0);
+    cr.shi = (uint64_t)a0 | (uint64_t)a1 << 32;
+    cr.slo = (uint64_t)a2 | (uint64_t)a3 << 32;
+    cr.buf = a4;
+    cr.has = a5;
+  }
+  CR[0] = CR[1] = CR[2] = 0u;
+  if (!c.kt_serial) {
+    const int m0 = k * sub / g, m1 = k * (sub + 1) / g;
+    // pass 1: the lane's multi-route cars (count, last one) and lane-less squares
+    int cnt = 0, lastf = -1, bad = 0;
+    for (int m = m0; m < m1; m += kCarChunk) {
+      CarSquare q[kCarChunk];
+      car_squares<kCarChunk>(c, pl, out, m, m1, q);
+#pragma unroll
+      for (int u = 0; u < kCarChunk; u++) {
+        if (m + u < m1) {
+          bad |= q[u].nr == 0u ? 1 : 0;
+          cnt += q[u].nr > 1u ? 1 : 0;
+          lastf = q[u].nr > 1u ? m + u : lastf;
+        }
+      }
+    }
+    int T = 0, prevf = -1;  // route draws before the lane's cars, the last multi-route car before them
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int src = q0 + (j < g ? j : 0);
+      const int a = __shfl(cnt, src), lf = __shfl(lastf, src), bd = __shfl(bad, src);
+      if (j < sub) {
+        T += a;
+        prevf = a > 0 ? lf : prevf;
+      }
+      if (j < g) bad |= bd;
+    }
+    if (bad) return PGTG_E_MAP;  // (the serial loop's error; cr stays the post-shuffle stream)
+    // route draw t takes the buffered half when t < B0, else t' = t - B0 even: a fresh output, odd: the
+    // buffered high half of draw t-1's output.  NC(t) = fresh outputs taken by draws 0 .. t-1.
+    const int B0 = (int)cr.has;
+    auto NC = [&](int t) { return t <= B0 ? 0 : (t - B0 + 1) >> 1; };
+    const int nbits = c.kt_jump_bits;
+    Pcg ls = cr;
+    ls.has = 0u;
+    if (T >= B0 && ((T - B0) & 1)) {  // the buffer holds the high half of the output of draw T-1
+      Pcg q = cr;
+      pcg_advance(q, (uint32_t)(prevf + 1 + NC(T - 1)), nbits);
+      ls.buf = (uint32_t)(pcg_next64(q) >> 32);
+      ls.has = 1u;
+    } else if (T < B0) {
+      ls.has = 1u;  // cr.buf
+    }
+    pcg_advance(ls, (uint32_t)(m0 + NC(T)), nbits);
+    // pass 2: this lane's cars
+    const ProfileCdf pcdf = pin_profile_cdf(c);
+    PcgAhead ca = ahead_init(ls);
+    int rej = 0;
+    uint64_t a_m = cs.at(m0);
+    for (int m = m0; m < m1; m += kCarChunk) {
+      CarSquare q[kCarChunk];
+      car_squares<kCarChunk>(c, pl, out, m, m1, q);
+      int prof[kCarChunk], lr[kCarChunk];
+#pragma unroll
+      for (int u = 0; u < kCarChunk; u++) {
+        uint32_t rk = 0u;
+        prof[u] = 0;
+        if (m + u < m1) {
+          if (q[u].tile == at) CR[q[u].sq >> 5] |= 1u << (q[u].sq & 31);
+          prof[u] = profile_of(pcdf, ahead_next64(ca) >> 11);
+          if (q[u].nr > 1u) {
+            const uint64_t mm = (uint64_t)ahead_next32(ca) * q[u].nr;
+            // a possible rejection (left < n; it is one iff left < 2^32 mod n): rare enough (n / 2^32)
+            // to send the group to the serial loop without computing the modulo
+            if ((uint32_t)mm < q[u].nr) rej = 1;
+            rk = (uint32_t)(mm >> 32);
+          }
+        }
+        lr[u] = max(select32(q[u].rl, (int)rk), 0);  // (a lane-less square of a clamped index reads row 0)
+      }
+      int route[kCarChunk];
+#pragma unroll
+      for (int u = 0; u < kCarChunk; u++) route[u] = sT.lane_route[lr[u]];
+#pragma unroll
+      for (int u = 0; u < kCarChunk; u++) {
+        if (m + u < m1) store_new_car(cs, a_m, q[u], route[u], prof[u], m + u);
+        a_m += cs.n;
+      }
+    }
+    ls = ca.g;
+    // the group's rejections; the stream after the last car is lane g-1's; CR merged on lane 0
+    const int last = q0 + g - 1;
+    uint32_t f0 = __shfl((uint32_t)ls.shi, last), f1 = __shfl((uint32_t)(ls.shi >> 32), last);
+    uint32_t f2 = __shfl((uint32_t)ls.slo, last), f3 = __shfl((uint32_t)(ls.slo >> 32), last);
+    uint32_t f4 = __shfl(ls.buf, last), f5 = __shfl(ls.has, last);
+    uint32_t cr0 = 0u, cr1 = 0u, cr2 = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int src = q0 + (j < g ? j : 0);
+      const uint32_t b0 = __shfl(CR[0], src), b1 = __shfl(CR[1], src), b2 = __shfl(CR[2], src);
+      const int rj = __shfl(rej, src);
+      if (j < g) {
+        cr0 |= b0;
+        cr1 |= b1;
+        cr2 |= b2;
+        rej |= rj;
+      }
+    }
+    if (!rej) {
+      CR[0] = cr0;
+      CR[1] = cr1;
+      CR[2] = cr2;
+      cr.shi = (uint64_t)f0 | (uint64_t)f1 << 32;
+      cr.slo = (uint64_t)f2 | (uint64_t)f3 << 32;
+      cr.buf = f4;
+      cr.has = f5;
+      return 0;
+    }
+  }
+  // one lane: the tune_kt_serial path, or a group whose draw positions a rejection shifted (redo)
+  return sub == 0 ? cars_serial(c, cs, pl, out, k, at, CR, cr) : 0;
+}
+
+// The draws of Generator.choice(np, k, replace=False) (numpy _generator.pyx: Floyd's loop over
+// j = np-k .. np-1 drawing integers(0, j+1), then _shuffle_int drawing integers(0, m+1) for m = k-1
+// .. 1), split over the g lanes of the env's group: draw d < k is Floyd's (n = np-k+d+1), d >= k the
+// shuffle's (n = 2k-d).  Every draw with n > 1 takes one 32-bit half of the car stream (next_uint32:
+// the low half of a fresh output, then its buffered high half), so draw d's half is known up front:
+// lane `sub` jumps its copy of the stream to its first draw and evaluates its stretch [D sub/g,
+// D (sub+1)/g) of the D = 2k-1 draws into out[d] / jj[d-k].  A Lemire rejection (left < 2^32 mod n)
+// takes an extra half and shifts every later draw by one: the group finds its first rejected draw and
+// re-evaluates from there with the shift, until none is left.  On return every lane holds the stream
+// after the last draw in `cr`.
+__device__ __forceinline__ void choice_draws_group(const DevCfg& c, uint16_t* out, uint16_t* jj, int np, int k, Pcg& cr,
+                                                   int sub, int g) {
+  const int q0 = (int)(threadIdx.x & 63u) - sub;
+  const int D = 2 * k - 1, da = D * sub / g, db = D * (sub + 1) / g;
+  const int z = np - k + 1 <= 1 ? 1 : 0;  // Floyd's first draw with n == 1 draws nothing
+  const int B = (int)cr.has;
+  const int nbits = c.kt_jump_bits + 1;
+  int shift = 0, dstart = 0;
+  Pcg ls = cr;
+  for (;;) {
+    const int d0 = max(da, dstart);
+    // the stream at the first half this lane takes: half h -> buffered (h < B) or output (h-B)/2
+    const int h0 = max(d0 - z, 0) + shift;
+    ls = cr;
+    if (h0 >= B) {
+      const int hb = h0 - B;
+      pcg_advance(ls, (uint32_t)(hb >> 1), nbits);
+      ls.has = 0u;
+      if (hb & 1) {  // the first draw takes the high half of output hb/2
+        ls.buf = (uint32_t)(pcg_next64(ls) >> 32);
+        ls.has = 1u;
+      }
+    }
+    int rej = 0x7fffffff;
+    for (int d = d0; d < db; d++) {
+      const uint32_t n = d < k ? (uint32_t)(np - k + d + 1) : (uint32_t)(2 * k - d);
+      uint32_t v = 0u;
+      if (n > 1u) {
+        const uint64_t mm = (uint64_t)pcg_next32(ls) * n;
+        const uint32_t left = (uint32_t)mm;
+        if (left < n && left < (0xffffffffu - (n - 1u)) % n && rej == 0x7fffffff) rej = d;
+        v = (uint32_t)(mm >> 32);
+      }
+      if (d < k) out[d] = (uint16_t)v;
+      else jj[d - k] = (uint16_t)v;
+    }
+    int first = rej;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int r = __shfl(rej, q0 + (j < g ? j : 0));
+      first = j < g ? min(first, r) : first;
+    }
+    if (first == 0x7fffffff) break;
+    dstart = first;  // draws before it stand; it and the later ones take one half more
+    shift++;
+  }
+  // the stream after the last draw: lane g-1's (its stretch ends at D; with an empty stretch, the
+  // jump above landed exactly there)
+  const int last = q0 + g - 1;
+  const uint32_t f0 = __shfl((uint32_t)ls.shi, last), f1 = __shfl((uint32_t)(ls.shi >> 32), last);
+  const uint32_t f2 = __shfl((uint32_t)ls.slo, last), f3 = __shfl((uint32_t)(ls.slo >> 32), last);
+  const uint32_t f4 = __shfl(ls.buf, last), f5 = __shfl(ls.has, last);
+  cr.shi = (uint64_t)f0 | (uint64_t)f1 << 32;
+  cr.slo = (uint64_t)f2 | (uint64_t)f3 << 32;
+  cr.buf = f4;
+  cr.has = f5;
+}
+
 // Initial traffic of a fresh episode (EpisodeMap scans pgtg/map.py:31-42 and
 // _create_initial_traffic pgtg/environment.py:830-879), run by k_traffic for the envs k_env reset.
 // `g` (1..4) adjacent lanes of a wave share one env (`sub` 0..g-1): lane 0 runs the serial parts
@@ -912,108 +1202,127 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
     k = min(ncars, np);
     if (k > c.car_cap) return PGTG_E_UNSUPPORTED;
     uint16_t* out = reinterpret_cast<uint16_t*>(rs);
-    if (sub == 0) {
-      uint32_t* seen = reinterpret_cast<uint32_t*>(rs + c.rs_seen_off);
+    uint16_t* jj = reinterpret_cast<uint16_t*>(rs + c.rs_jj_off);
+    uint32_t* seen = reinterpret_cast<uint32_t*>(rs + c.rs_seen_off);
+    if (sub == 0)
       for (int w = 0; w < (np + 31) / 32; w++) seen[w] = 0u;
-      STAMP(20);
-      // Generator.choice(np, k, replace=False): Floyd's algorithm, then _shuffle_int
-      PcgAhead ca = ahead_init(cr);
-      for (int j = np - k; j < np; j++) {
-        int val = (int)ahead_int(ca, (uint32_t)(j + 1));
+    STAMP(20);
+    // Generator.choice(np, k, replace=False): Floyd's algorithm, then _shuffle_int.  Their draws
+    // (values independent of the outcomes) are evaluated lane-parallel into out / jj
+    // (choice_draws_group); the set and swap bookkeeping stays in order on lane 0.
+    choice_draws_group(c, out, jj, np, k, cr, sub, g);
+    wave_lds_sync();
+    if (sub == 0) {
+      for (int d = 0; d < k; d++) {
+        const int j = np - k + d;
+        int val = out[d];
         if ((seen[val >> 5] >> (val & 31)) & 1u) val = j;
         seen[val >> 5] |= 1u << (val & 31);
-        out[j - (np - k)] = (uint16_t)val;
+        out[d] = (uint16_t)val;
       }
       STAMP(21);
       for (int m = k - 1; m >= 1; m--) {
-        int jj = (int)ahead_int(ca, (uint32_t)(m + 1));
-        const uint16_t t = out[m], u = out[jj];
+        const int q = jj[k - 1 - m];
+        const uint16_t t = out[m], u = out[q];
         out[m] = u;
-        out[jj] = t;
+        out[q] = t;
       }
-      cr = ca.g;
     }
     wave_lds_sync();
     STAMP(22);
     const int tw = c.tw, th = c.th;
-    // the group looks up the squares: chosen index -> square code x | y << 8 in place
-    for (int m = sub; m < k; m += g) {
-      const int idx = out[m];
-      // column: the tile column from the prefixes at tile-column starts, then the column inside it
-      int tx = 0;
-      for (int q = 1; q < tw; q++) tx += colpre[q * kTile] <= idx ? 1 : 0;
-      const uint16_t* cp = colpre + tx * kTile;
-      int lx = 0;
+    // the group looks up the squares: chosen index -> square code x | y << 8 in place, lane `sub` on
+    // indices [k sub/g, k (sub+1)/g), kCarChunk at a time (each level's LDS reads issued together)
+    const int la = k * sub / g, lb = k * (sub + 1) / g;
+    for (int m = la; m < lb; m += kCarChunk) {
+      int idx[kCarChunk], tx[kCarChunk];
 #pragma unroll
-      for (int j = 1; j < kTile; j++) lx += cp[j] <= idx ? 1 : 0;
-      // row: the tile of the column holding the rr-th spawnable square (no early exit)
-      int rr = idx - cp[lx];
-      const int x = tx * kTile + lx;
-      int y;
-      if (colm) {  // the rr-th set bit of the column mask
-        uint32_t w = colm[2 * x];
-        const uint32_t hi = colm[2 * x + 1];
-        int base = 0;
-        const int c32 = __popc(w);
-        if (rr >= c32) {
-          rr -= c32;
-          w = hi;
-          base = 32;
-        }
-#pragma unroll
-        for (int sh = 16; sh >= 1; sh >>= 1) {
-          const int cs = __popc(w & ((1u << sh) - 1u));
-          if (rr >= cs) {
-            rr -= cs;
-            w >>= sh;
-            base += sh;
-          }
-        }
-        y = base;
-      } else {  // row: the tile of the column holding the rr-th spawnable square (no early exit)
-        int ty_f = 0, rr_f = 0;
-        uint32_t msk_f = 0;
-        for (int ty = 0; ty < th; ty++) {
-          const uint32_t msk = sT.lanecol[plan_exits(pl[ty * tw + tx])][lx];
-          const int cnt = __popc(msk);
-          if (rr >= 0 && rr < cnt) {
-            ty_f = ty;
-            msk_f = msk;
-            rr_f = rr;
-          }
-          rr -= cnt;
-        }
-        y = ty_f * kTile + kth_bit(msk_f, rr_f);
+      for (int u = 0; u < kCarChunk; u++) {
+        idx[u] = out[min(m + u, lb - 1)];
+        tx[u] = 0;
       }
-      out[m] = (uint16_t)(x | y << 8);
+      // column: the tile column from the prefixes at tile-column starts, then the column inside it
+      for (int q = 1; q < tw; q++) {
+        const int cv = colpre[q * kTile];
+#pragma unroll
+        for (int u = 0; u < kCarChunk; u++) tx[u] += cv <= idx[u] ? 1 : 0;
+      }
+      int cpv[kCarChunk][kTile];
+#pragma unroll
+      for (int u = 0; u < kCarChunk; u++)
+#pragma unroll
+        for (int j = 0; j < kTile; j++) cpv[u][j] = colpre[tx[u] * kTile + j];
+      int x[kCarChunk], rr[kCarChunk];
+#pragma unroll
+      for (int u = 0; u < kCarChunk; u++) {
+        int lx = 0, base = cpv[u][0];
+#pragma unroll
+        for (int j = 1; j < kTile; j++) {
+          const bool le = cpv[u][j] <= idx[u];
+          lx += le ? 1 : 0;
+          base = le ? cpv[u][j] : base;
+        }
+        x[u] = tx[u] * kTile + lx;
+        rr[u] = idx[u] - base;
+      }
+      int y[kCarChunk];
+      if (colm) {  // row: the rr-th set bit of the column's row mask
+        uint32_t wl[kCarChunk], wh[kCarChunk];
+#pragma unroll
+        for (int u = 0; u < kCarChunk; u++) {
+          wl[u] = colm[2 * x[u]];
+          wh[u] = colm[2 * x[u] + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < kCarChunk; u++) {
+          uint32_t w = wl[u];
+          int r = rr[u], base = 0;
+          const int c32 = __popc(w);
+          if (r >= c32) {
+            r -= c32;
+            w = wh[u];
+            base = 32;
+          }
+#pragma unroll
+          for (int sh = 16; sh >= 1; sh >>= 1) {
+            const int cnt = __popc(w & ((1u << sh) - 1u));
+            if (r >= cnt) {
+              r -= cnt;
+              w >>= sh;
+              base += sh;
+            }
+          }
+          y[u] = base;
+        }
+      } else {  // row: the tile of the column holding the rr-th spawnable square (no early exit)
+#pragma unroll
+        for (int u = 0; u < kCarChunk; u++) {
+          const int txu = x[u] / kTile, lx = x[u] - txu * kTile;
+          int ty_f = 0, rr_f = 0, r = rr[u];
+          uint32_t msk_f = 0;
+          for (int ty = 0; ty < th; ty++) {
+            const uint32_t msk = sT.lanecol[plan_exits(pl[ty * tw + txu])][lx];
+            const int cnt = __popc(msk);
+            if (r >= 0 && r < cnt) {
+              ty_f = ty;
+              msk_f = msk;
+              rr_f = r;
+            }
+            r -= cnt;
+          }
+          y[u] = ty_f * kTile + kth_bit(msk_f, rr_f);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kCarChunk; u++)
+        if (m + u < lb) out[m + u] = (uint16_t)(x[u] | y[u] << 8);
     }
     wave_lds_sync();
     STAMP(26);  // (slot shared with k_env's removal-loop record: k_traffic runs later)
+    // the cars in id order: profile and route draws -> slots 0 .. k-1 (lane-parallel, see cars_group)
+    const int e = cars_group(c, cs, pl, out, k, at, CR, cr, sub, g);
+    if (e) return sub == 0 ? e : 0;
     if (sub != 0) return 0;
-    // the cars in id order: profile and route draws -> slots 0 .. k-1
-    const ProfileCdf pcdf = pin_profile_cdf(c);
-    PcgAhead ca = ahead_init(cr);
-    uint64_t a_m = cs.at(0);  // slot index, advanced by the env stride
-    for (int m = 0; m < k; m++) {
-      const uint32_t code = out[m];
-      const int x = (int)(code & 255u), y = (int)(code >> 8);
-      const int tx = (int)((uint32_t)x / (uint32_t)kTile), ty_f = (int)((uint32_t)y / (uint32_t)kTile);
-      const int lx = x - tx * kTile, ly = y - ty_f * kTile, sq = lx * 9 + ly;
-      const uint32_t ex_f = plan_exits(pl[ty_f * tw + tx]);
-      if (ty_f * tw + tx == at) CR[sq >> 5] |= 1u << (sq & 31);
-      const uint32_t rl = sT.lanes[ex_f][sq] & 0x0fffffffu;
-      const uint32_t nr = __popc(rl);
-      if (nr == 0) return PGTG_E_MAP;  // "a car was spawned on a field where no car lane was found"
-      const uint64_t u = ahead_draw(ca, false, 0u);
-      const int prof = profile_of(pcdf, u);
-      const uint32_t rk = nr > 1u ? (uint32_t)ahead_draw(ca, true, nr) : 0u;
-      const int route = sT.lane_route[kth_bit(rl, (int)rk)];
-      cs.w0[a_m] = (uint32_t)x | (uint32_t)y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
-      cs.w1[a_m] = 0u;
-      cs.id[a_m] = (uint32_t)m;
-      a_m += N;
-    }
-    cr = ca.g;
   }
   STAMP(23);
   ts.n_cars = (uint32_t)k;
@@ -2139,7 +2448,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       ts.next_id = tr4.y;
       ts.tail = tr4.z;
     }
-    stage_plan(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, L.plan_stride_dw);
+    stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, L.plan_stride_dw);
   }
   for (int k = tid; k < L.lm_words; k += kBlock) lm[k] = 0u;
   lds_barrier();  // sT ready
@@ -2478,7 +2787,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     v = rec_load(S.rec, i);
     qs = S.qstate[i];
     act = actions[i];  // issued with the staging loads, not on the step's chain
-    stage_plan(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, pdw);
+    stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, pdw);
     xf[slot * L.scratch_dw] = v.spawn;
     xf[slot * L.scratch_dw + 1] = qs;
   }
@@ -2732,7 +3041,8 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
     const uint32_t j = (r * W + blockIdx.x * (kBlock / 64) + (uint32_t)wave) * e + (uint32_t)slot;
     if (j >= n) break;
     const uint64_t i = S.tr_list[j];
-    stage_plan(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, plan_dw);
+    if (c.nt > kSmallTiles) stage_plan<true>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, plan_dw);
+    else stage_plan<false>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, plan_dw);
     Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
     const EnvView v = rec_load(S.rec, i);
     const int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
@@ -3156,6 +3466,12 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
     if (cap < in.min_car_capacity) cap = in.min_car_capacity;
     if (cap < 1) cap = 1;
     c.car_cap = cap;
+    // initial traffic consumes <= 1 + 2 cap outputs of the car stream after the shuffle (a profile
+    // double and a route draw per car)
+    c.kt_jump_bits = 1;
+    while ((2 * cap + 2) >> c.kt_jump_bits) c.kt_jump_bits++;
+    if (c.kt_jump_bits > kJumpBits) return fail(h, PGTG_E_UNSUPPORTED, "car capacity above the jump-ahead table");
+    c.kt_serial = in.tune_kt_serial != 0;
     // one bank: a tick starts with at most 2 x cap + kCompactSlack slots in use (a tick that does not
     // pack starts with <= cap + kCompactSlack and appends <= cap respawns) and appends <= cap more
     c.car_slots = 3 * cap + kCompactSlack;  // configs[2]: 1 204 slots x 12 B x 65 536 envs = 947 MB
@@ -3167,8 +3483,10 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
     // k_env: occupancy counters (nt * 32 lane slots, 4 bit) then the spawner cache
     c.sp_cache_off = c.nt * 16;
     c.traf_bytes = c.sp_cache_off + 2 * kSpCache;
-    // k_traffic: Floyd output (u16 x cap), seen bits of the spawnable squares (<= nt * 32), column prefix
-    c.rs_seen_off = ((2 * cap + 3) / 4) * 4;
+    // k_traffic: Floyd output (u16 x cap), the shuffle's draws (u16 x cap), seen bits of the spawnable
+    // squares (<= nt * 32), column prefix
+    c.rs_jj_off = ((2 * cap + 3) / 4) * 4;  // the shuffle's draws (u16 x cap)
+    c.rs_seen_off = c.rs_jj_off + ((2 * cap + 3) / 4) * 4;
     c.rs_pre_off = c.rs_seen_off + 4 * c.nt;
     c.rs_bytes = (c.rs_pre_off + 2 * (c.W + 1) + 3) / 4 * 4;
     c.rs_cm_off = 0;

@@ -1,7 +1,9 @@
 """k_traffic's launch shapes against the CPU oracle: the work list is levelled over the grid's waves
 (`e` envs per wave, in rounds beyond the LDS capacity `cap`) and each env gets 4, 3 or 2 lanes by `e`
 (pgtg_env.hip k_traffic / traffic_reset).  The launch-shape overrides tune_kt_grid / tune_kt_cap force every
-shape with small batches: quads, triples, pairs, one env per wave in many rounds."""
+shape with small batches: quads, triples, pairs, one env per wave in many rounds.  The per-car draws
+of the initial traffic run lane-parallel (cars_group: each lane jumps the env's car stream to its
+cars); tune_kt_serial forces the one-lane loop that a Lemire rejection falls back to."""
 
 import numpy as np
 import pytest
@@ -24,15 +26,20 @@ SHAPES = {
     # more than seven tile rows: the lookup's per-tile row search instead of the column row masks
     "tall_map": (256, 8, None, (2, 9)),
     "wide_map": (256, 8, None, (9, 2)),
+    # the per-car draws on one lane per env (the rejection fallback of cars_group)
+    "serial_quads_e16": (512, 8, None, (5, 5), {"kt_serial": 1}),
+    "serial_pairs_e25": (800, 8, None, (5, 5), {"kt_serial": 1}),
 }
 
 
 @pytest.mark.parametrize("name", sorted(SHAPES))
 def test_traffic_launch_shapes(name):
     from pgtg_amd.vector import PGTGVecEnv
-    n, grid, cap, (mw, mh) = SHAPES[name]
+    n, grid, cap, (mw, mh), *extra = SHAPES[name]
     spec = cfg.make_spec(random_map_width=mw, random_map_height=mh, traffic_density=0.5)
     tune = {"kt_grid": grid} if cap is None else {"kt_grid": grid, "kt_cap": cap}
+    if extra:
+        tune.update(extra[0])
     env = PGTGVecEnv(n, spec=spec, device=0, tune=tune)
     rng = np.random.default_rng(n)
     idx = np.unique(np.concatenate([[0, 1, 2, n // 2, n - 2, n - 1], rng.choice(n, 12, replace=False)]))

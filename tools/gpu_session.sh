@@ -16,6 +16,7 @@
 #   ab:<wl>:<lib>    interleaved bench lines of the in-tree library and <lib> (tools/ab_multi.sh, 3 reps)
 #   libtests:<lib>:<expr>  pytest -m gpu -k <expr> against another build of the library (PGTG_LIB)
 #   pmc:<wl>:<lib|new>     FETCH_SIZE / WRITE_SIZE passes of one workload with a given library
+#   sq:<wl>          SQ instruction/stall passes of one workload -> gpurun_out/<tag>/sq_<wl>.json (issue roofline)
 set -o pipefail
 TAG=$1
 shift
@@ -79,6 +80,12 @@ for S in "$@"; do
       R=${S#ab:}; W=${R%%:*}; L=${R#*:}
       timeout -k 10 900 bash tools/ab_multi.sh $W 3 new $L > $O/ab_$W.log 2>&1 || { tail -20 $O/ab_$W.log; exit 1; }
       cat $O/ab_$W.log ;;
+    sq:*)
+      W=${S#sq:}
+      timeout -k 10 300 bash tools/sq_passes.sh $TAG $W > $O/sq_$W.log 2>&1 || { tail -20 $O/sq_$W.log; exit 1; }
+      N=$(python -c "import bench; print(bench.WORKLOADS['$W'][2])")
+      python tools/sq_json.py $W $N gpurun_out/sq_$TAG/$W/p1 gpurun_out/sq_$TAG/$W/p2 > $O/sq_$W.json || exit 1
+      python tools/sq_summary.py k_ gpurun_out/sq_$TAG/$W/p1 gpurun_out/sq_$TAG/$W/p2 ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done
