@@ -157,6 +157,8 @@ def main():
     ap.add_argument("--digest-steps", type=int, default=8)
     ap.add_argument("--per-step", action="store_true", help="A/B: one pgtg_step host call per timed step")
     ap.add_argument("--envs-per-block", type=int, default=0, help="A/B: force the step kernel's envs per workgroup")
+    ap.add_argument("--kt-wpc", type=int, default=0, help="A/B: k_traffic workgroups per CU")
+    ap.add_argument("--kt-cap", type=int, default=0, help="A/B: k_traffic envs per wave held in LDS")
     args = ap.parse_args()
 
     import torch
@@ -191,7 +193,8 @@ def main():
     spec = make_spec(**kwargs)
     shard = Shard(rank, world, n_local)
     peak_copy = measure_hbm(local) if rank == 0 else 0.0
-    tune = {"envs_per_block": args.envs_per_block} if args.envs_per_block else None
+    tune = {k: v for k, v in (("envs_per_block", args.envs_per_block), ("kt_wpc", args.kt_wpc),
+                              ("kt_cap", args.kt_cap)) if v} or None
     env = PGTGVecEnv(n_local, spec=spec, device=local, autoreset=True, tune=tune)
     env.reset(seed=shard.offset)  # global env g = rank*n_local + i gets seed g
     act_seed = 0x5EED

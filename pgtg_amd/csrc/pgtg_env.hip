@@ -101,9 +101,19 @@ __device__ unsigned long long g_stamps[1 << 21];
       g_stamps[((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 32 + (k)) & ((1 << 21) - 1)] = t_; \
     }                                                                                     \
   } while (0)
+// wall-clock (s_memrealtime, 100 MHz, one clock for the chip) stamp k in {0, 1} of the wave
+#define STAMPR(k)                                                                                     \
+  do {                                                                                                \
+    if ((threadIdx.x & 63) == 0)                                                                      \
+      g_stamps[(1 << 20) | ((((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 8 + (k))) & ((1 << 20) - 1))] = \
+          __builtin_amdgcn_s_memrealtime();                                                           \
+  } while (0)
 #else
 #define STAMP(k) \
   do {           \
+  } while (0)
+#define STAMPR(k) \
+  do {            \
   } while (0)
 #endif
 
@@ -330,11 +340,17 @@ __device__ __forceinline__ int profile_of(const ProfileCdf& p, uint64_t u) {
 }
 
 constexpr uint32_t kCarEmpty = 1u << 31;  // w0 of a slot without a car
-struct CarSlots {  // one env's car slots (DevState::car_w0 layout): slot k of env i at k * n + i
+// One env's car slots (DevState::car_w0 layout: slot k of env i at k * n + i) through per-lane
+// pointers at the env's slot 0: the three array bases stay in VGPRs instead of being re-read from
+// spilled scalar registers at every access of the car loops.
+struct CarSlots {
   uint32_t *w0, *w1, *id;
   uint64_t n;  // stride between slots (= number of envs)
-  uint64_t i;  // env index
-  __device__ __forceinline__ uint64_t at(int k) const { return (uint64_t)k * n + i; }
+  __device__ __forceinline__ CarSlots(const DevState& S, uint64_t i)
+      : w0(S.car_w0 + i), w1(S.car_w1 + i), id(S.car_id + i), n(S.n) {
+    __asm__ volatile("" : "+v"(w0), "+v"(w1), "+v"(id));
+  }
+  __device__ __forceinline__ uint64_t at(int k) const { return (uint64_t)k * n; }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -1197,7 +1213,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
   wave_lds_sync();
   const int ncars = (int)((double)np * c.density);  // int(len(positions) * traffic_density)
   int k = 0;
-  const CarSlots cs{S.car_w0, S.car_w1, S.car_id, N, i};
+  const CarSlots cs(S, i);
   if (ncars > 0 && np > 0) {
     k = min(ncars, np);
     if (k > c.car_cap) return PGTG_E_UNSUPPORTED;
@@ -1711,7 +1727,7 @@ constexpr int kCompactSlack = PGTG_SLACK;
 __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uint64_t i, const EnvView& v,
                                          const Plan& pl, uint8_t* occ, bool& sat, const uint16_t* sp, TrafState& ts,
                                          Pcg& cr, int color, BrakeQuery& bq, uint8_t* hist) {
-  const CarSlots cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
+  const CarSlots cs(S, i);
   const int tw = c.tw, th = c.th;
   const uint32_t nsp = ts.n_spawners;
   const int tail0 = (int)ts.tail;
@@ -2456,7 +2472,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     // occupancy counters from the current car positions (one coalesced slot row per slot index, 16
     // loads in flight per lane)
     for (int w = 0; w < c.nt * 4; w++) traf_w[w] = 0u;  // 16 B of 4-bit counters per tile
-    const CarSlots cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
+    const CarSlots cs(S, i);
     const int tail = (int)ts.tail, tw = pinned(c.tw);
     for (int k0 = 0; k0 < tail; k0 += 16) {
       uint32_t a16[16];
@@ -2644,6 +2660,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (mode == MODE_STEP && tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
   if (!TR) stagger_record(L, S, t_start);
   STAMP(6);
+  if (TR) STAMPR(0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3021,6 +3038,8 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
                                                     DevState S, PgtgOutputs out, uint32_t tr_slot, int plan_dw,
                                                     int rs_dw, int cap_w) {
   extern __shared__ uint32_t lds[];
+  STAMP(27);  // (k_traffic's wave start and end: slots 27 and 24, after k_env's last use of them)
+  STAMPR(1);
   const DevCfg& c = *cfg;
   const uint32_t n = S.tr_count[tr_slot];
   const uint32_t W = gridDim.x * (kBlock / 64);  // waves of the grid
@@ -3033,6 +3052,12 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
   const int slot = lane / g, sub = lane - slot * g;
   stage_tables(gtab, (int)sizeof(Tables));
   __syncthreads();
+  STAMP(25);
+#ifdef PGTG_STAMPS
+  if ((threadIdx.x & 63) == 0)  // the launch's shape (last launch): list length, rounds, envs per wave, capacity
+    g_stamps[((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 32 + 15) & ((1 << 21) - 1)] =
+        (unsigned long long)n | (unsigned long long)rounds << 32 | (unsigned long long)e << 40 | (unsigned long long)cap_w << 48;
+#endif
   if ((uint32_t)slot >= e) return;
   const int ls = wave * cap_w + slot;  // LDS slot of the env
   uint32_t* plan_w = lds + ls * plan_dw;
@@ -3071,6 +3096,7 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
     }
     wave_lds_sync();  // the group's scratch is reused by the next round
   }
+  STAMP(24);
 }
 
 // Feature words of every square of env i's map (introspection: get_info, tests); one workgroup.
@@ -3155,7 +3181,7 @@ __global__ void __launch_bounds__(256) k_car_digest(DevState S, uint64_t* __rest
   if (i >= S.n) return;
   constexpr uint64_t CB = 1ull << 40;
   const uint4 t = S.traf[i];
-  const CarSlots cs{S.car_w0, S.car_w1, S.car_id, S.n, i};
+  const CarSlots cs(S, i);
   uint64_t d = (uint64_t)(t.x & 0xffffu) * dg_w(CB), j = 0;
   for (int k = 0; k < (int)t.z; k++) {
     const uint32_t w0 = cs.w0[cs.at(k)];

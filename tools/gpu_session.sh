@@ -6,6 +6,7 @@
 #   smoke            __graft_entry__.smoke()
 #   bench            the default bench line (configs[4], with the CPU baseline)
 #   bench:<wl>       bench.py --workload <wl> --steps 200 --warmup 20
+#   benchlong:<wl>   bench.py --workload <wl> with the default 1000-step window
 #   rccl             bench.py under torch.distributed.run, one rank, nccl backend, --dist (RCCL init +
 #                    the device counter all-reduce), 131 072 envs
 #   shards           single-process lines at the per-rank shards of N = 2, 4, 8 (524 288 / 262 144 /
@@ -38,6 +39,10 @@ for S in "$@"; do
     bench)
       timeout -k 10 400 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
       cat $O/bench_default.json ;;
+    benchlong:*)
+      W=${S#benchlong:}
+      timeout -k 10 400 python -u bench.py --workload $W --no-cpu-baseline > $O/benchlong_$W.json 2> $O/benchlong_$W.err || { tail -20 $O/benchlong_$W.err; exit 1; }
+      python tools/bench_line.py $O/benchlong_$W.json ;;
     bench:*)
       W=${S#bench:}
       timeout -k 10 300 python -u bench.py --workload $W --steps 200 --warmup 20 --no-cpu-baseline > $O/bench_$W.json 2> $O/bench_$W.err || { tail -20 $O/bench_$W.err; exit 1; }

@@ -41,13 +41,15 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
     env.reset(seed=0)
     for k in range(int(os.environ.get("PGTG_STAMP_STEPS", "30"))):
         env.step_random(1, k)
+        if os.environ.get("PGTG_STAMP_SYNC") == "1":
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     blocks = (N + E - 1) // E
     nw = blocks * 4
-    buf = np.zeros(nw * SLOTS, np.uint64)
+    buf = np.zeros(max(nw * SLOTS, (1 << 20) + 8 * nw), np.uint64)
     _abi.lib().pgtg_read_stamps.argtypes = [C.c_void_p, C.c_uint64]
     _abi.lib().pgtg_read_stamps(buf.ctypes.data, buf.size)
-    st = buf.reshape(nw, SLOTS).astype(np.int64)
+    st = buf[:nw * SLOTS].reshape(nw, SLOTS).astype(np.int64)
     # traffic workgroups spread their env slots over all four waves; otherwise envs fill waves in order
     spread = kw.get("traffic_density", 0) > 0
     active = np.ones(nw, bool) if spread else (np.arange(nw) % 4) * 64 < E
@@ -75,6 +77,25 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
         if ok.any():
             out[n] = (int((st[ok, b] - st[ok, a]).mean()), round(float(ok.mean()), 2))
     print("  sub-phases (mean cycles, fraction of waves):", out, flush=True)
+    if spread:  # k_traffic waves: start (slot 27) to end (slot 24), start spread over the grid
+        ok = (st[:, 27] > 0) & (st[:, 24] > st[:, 27]) & (st[:, 24] - st[:, 27] < 1e9)
+        if ok.any():
+            tot = st[ok, 24] - st[ok, 27]
+            t0 = st[ok, 27] - st[ok, 27].min()
+            pro = st[ok, 19] - st[ok, 27]
+            epi = st[ok, 24] - st[ok, 23]
+            body = st[ok, 23] - st[ok, 19]
+            q = lambda a: (int(a.mean()), int(np.percentile(a, 90)), int(a.max()))  # noqa: E731
+            rt = buf[1 << 20:(1 << 20) + 8 * nw].reshape(nw, 8).astype(np.int64)
+            e_end, t_beg = rt[:, 0], rt[rt[:, 1] > 0, 1]
+            print("  wall clock (10 ns ticks): k_env waves end", 0, "..", int(e_end.max() - e_end.min()),
+                  "; k_traffic waves start", int(t_beg.min() - e_end.min()), "..", int(t_beg.max() - e_end.min()), flush=True)
+            dv = st[ok, 15]  # the last launch's shape (k_traffic writes it over k_env's slot)
+            print("  k_traffic (last launch): list", int(dv[0] & 0xffffffff), "rounds", int((dv[0] >> 32) & 255),
+                  "envs per wave", int((dv[0] >> 40) & 255), "LDS capacity per wave", int((dv[0] >> 48) & 255),
+                  "(the traffic_reset stamps are the last round's)", flush=True)
+            print("  k_traffic waves (mean, p90, max): total", q(tot), "before the last round", q(pro),
+                  "last round's traffic_reset", q(body), "epilogue", q(epi), flush=True)
     if not spread:  # k_envq env waves: the observation channel loop's split (slots 24, 25)
         okc = (st[:, 24] > 0) & (st[:, 24] < 1e7) & (st[:, 25] < 1e7)
         if okc.any():
