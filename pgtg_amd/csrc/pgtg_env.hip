@@ -1735,7 +1735,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
   // exec-mask juggling around the packing writes)
   const bool pack = __any(tail0 > (int)ts.n_cars + kCompactSlack);
   const ProfileCdf pcdf = pin_profile_cdf(c);
-  PcgAhead ca = ahead_init(cr);
+  Pcg& ca = cr;
   int t_out = tail0, w = 0;
   const uint64_t nst = S.n;
   // software pipeline: the next slot's words are requested before the current car is processed, so
@@ -1809,8 +1809,8 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       const bool act = delay == 0;
       bool delayed = false, move = false;
       if (act) {
-        delayed = ahead_draw(ca, false, 0u) < th_delay;
-        const uint64_t r2 = ahead_draw(ca, delayed, 3u);
+        delayed = pcg_draw(ca, false, 0u) < th_delay;
+        const uint64_t r2 = pcg_draw(ca, delayed, 3u);
         if (delayed) delay = 1 + (int)r2;  // integers(1, 4)
         else move = r2 < th_speed;
       } else {
@@ -1823,11 +1823,11 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       const bool s3_int = kind != 2;
       const uint32_t s3_n = kind == 1 ? nr_all : nsp;
       uint64_t r3 = 0;
-      if ((kind == 1 || kind == 3 || lit) && !(s3_int && s3_n <= 1u)) r3 = ahead_draw(ca, s3_int, s3_n);
+      if ((kind == 1 || kind == 3 || lit) && !(s3_int && s3_n <= 1u)) r3 = pcg_draw(ca, s3_int, s3_n);
       const bool stop = lit && (color == 1 ? r3 < th_yellow : !(r3 < th_red));
       const bool go_try = kind == 2 && !stop && occ_tg > 0 && (b_mf == 0 || (int)pat > b_pt);
       uint64_t r4 = 0;
-      if (go_try || kind == 3) r4 = ahead_draw(ca, false, 0u);
+      if (go_try || kind == 3) r4 = pcg_draw(ca, false, 0u);
       const bool leaves = kind == 3 || kind == 1 || (kind == 2 && !stop && (occ_tg == 0 || (go_try && r4 < th_go)));
       if (leaves) {  // the car's square loses it
         if (sat && occ_get(occ, s_old) >= kOccMax) {
@@ -1849,7 +1849,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
         const uint32_t nr = __popc(rl);
         const int nprof = profile_of(pcdf, r4);
         if (nr == 0) return PGTG_E_MAP;
-        const uint32_t r5 = nr > 1u ? (uint32_t)ahead_draw(ca, true, nr) : 0u;
+        const uint32_t r5 = nr > 1u ? (uint32_t)pcg_draw(ca, true, nr) : 0u;
         const int nroute = sT.lane_route[kth_bit(rl, (int)r5)];
         if (!pack) cs.w0[aw] = kCarEmpty;
         cs.w0[an] = (uint32_t)sx | (uint32_t)sy << 8 | (uint32_t)nroute << 16 | (uint32_t)nprof << 21;
@@ -1903,7 +1903,6 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
     }
     t_out = w + (t_out - tail0);
   }
-  cr = ca.g;
   ts.tail = (uint32_t)t_out;
   return 0;
 }
@@ -2470,14 +2469,20 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   lds_barrier();  // sT ready
   if (live && (TR && c.need_car)) {
     // occupancy counters from the current car positions (one coalesced slot row per slot index, 16
-    // loads in flight per lane)
+    // loads in flight per lane, the next 16 requested before the counters of the current ones are
+    // updated so that their HBM latency overlaps the LDS work)
     for (int w = 0; w < c.nt * 4; w++) traf_w[w] = 0u;  // 16 B of 4-bit counters per tile
     const CarSlots cs(S, i);
     const int tail = (int)ts.tail, tw = pinned(c.tw);
+    uint32_t nx16[16];
+#pragma unroll
+    for (int g = 0; g < 16; g++) nx16[g] = cs.w0[cs.at(g < tail ? g : 0)];
     for (int k0 = 0; k0 < tail; k0 += 16) {
       uint32_t a16[16];
 #pragma unroll
-      for (int g = 0; g < 16; g++) a16[g] = cs.w0[cs.at(k0 + g < tail ? k0 + g : 0)];
+      for (int g = 0; g < 16; g++) a16[g] = nx16[g];
+#pragma unroll
+      for (int g = 0; g < 16; g++) nx16[g] = cs.w0[cs.at(k0 + 16 + g < tail ? k0 + 16 + g : 0)];
       // the 16 slot lookups first (every slot holds valid coordinates: empty slots read as (0, 0),
       // slots past the tail as slot 0), their reads batched; then the counter updates in order
       int sl[16];
