@@ -3683,10 +3683,11 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
     const void* fn = step_fn(h, MODE_STEP);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, h->lds) != hipSuccess || per_cu < 1) per_cu = 1;
     h->L.stagger_wgs = ncu * per_cu;
-    // only launches of several rounds: one round has no later workgroups to keep the offsets
-    // (1 048 576 5x5 envs, 8 rounds: k_envq 476 -> 460 us; one round: slower)
+    // only launches of two rounds or more: one round has no later workgroups to keep the offsets
+    // (1 048 576 5x5 envs, 8 rounds: k_envq 476 -> 460 us; 262 144 envs, 2 rounds: 140 -> 133 us;
+    // one round: 66 -> 78 us, profiles/r03/abrec/stagger_by_shard.txt)
     const uint64_t blocks = (h->n + h->L.envs - 1) / h->L.envs;
-    h->L.stagger = blocks >= (uint64_t)3 * h->L.stagger_wgs ? 1 : 0;
+    h->L.stagger = blocks >= (uint64_t)2 * h->L.stagger_wgs ? 1 : 0;
 #ifdef PGTG_TUNING
     if (const char* e = getenv("PGTG_STAGGER")) h->L.stagger = atoi(e);
 #endif
