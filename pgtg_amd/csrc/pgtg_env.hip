@@ -875,6 +875,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // One car of the initial traffic (pgtg/environment.py:840-879): square code -> lanes of the square
 constexpr int kCarChunk = 4;  // cars whose lookups cars_group issues together
+constexpr int kMaxGroup = 16;  // lanes of a wave that share one env in k_traffic
 struct CarSquare {
   int x, y, tile, sq;
   uint32_t rl, nr;  // route lanes (kLanes bits 0..27) and their count
@@ -983,15 +984,14 @@ __device__ __forceinline__ int cars_group(const DevCfg& c, const CarSlots& cs, c
       }
     }
     int T = 0, prevf = -1;  // route draws before the lane's cars, the last multi-route car before them
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int src = q0 + (j < g ? j : 0);
+    for (int j = 0; j < g; j++) {
+      const int src = q0 + j;
       const int a = __shfl(cnt, src), lf = __shfl(lastf, src), bd = __shfl(bad, src);
       if (j < sub) {
         T += a;
         prevf = a > 0 ? lf : prevf;
       }
-      if (j < g) bad |= bd;
+      bad |= bd;
     }
     if (bad) return PGTG_E_MAP;  // (the serial loop's error; cr stays the post-shuffle stream)
     // route draw t takes the buffered half when t < B0, else t' = t - B0 even: a fresh output, odd: the
@@ -1052,17 +1052,12 @@ __device__ __forceinline__ int cars_group(const DevCfg& c, const CarSlots& cs, c
     uint32_t f2 = __shfl((uint32_t)ls.slo, last), f3 = __shfl((uint32_t)(ls.slo >> 32), last);
     uint32_t f4 = __shfl(ls.buf, last), f5 = __shfl(ls.has, last);
     uint32_t cr0 = 0u, cr1 = 0u, cr2 = 0u;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int src = q0 + (j < g ? j : 0);
-      const uint32_t b0 = __shfl(CR[0], src), b1 = __shfl(CR[1], src), b2 = __shfl(CR[2], src);
-      const int rj = __shfl(rej, src);
-      if (j < g) {
-        cr0 |= b0;
-        cr1 |= b1;
-        cr2 |= b2;
-        rej |= rj;
-      }
+    for (int j = 0; j < g; j++) {
+      const int src = q0 + j;
+      cr0 |= __shfl(CR[0], src);
+      cr1 |= __shfl(CR[1], src);
+      cr2 |= __shfl(CR[2], src);
+      rej |= __shfl(rej, src);
     }
     if (!rej) {
       CR[0] = cr0;
@@ -1126,11 +1121,7 @@ __device__ __forceinline__ void choice_draws_group(const DevCfg& c, uint16_t* ou
       else jj[d - k] = (uint16_t)v;
     }
     int first = rej;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int r = __shfl(rej, q0 + (j < g ? j : 0));
-      first = j < g ? min(first, r) : first;
-    }
+    for (int j = 0; j < g; j++) first = min(first, __shfl(rej, q0 + j));
     if (first == 0x7fffffff) break;
     dstart = first;  // draws before it stand; it and the later ones take one half more
     shift++;
@@ -1149,7 +1140,7 @@ __device__ __forceinline__ void choice_draws_group(const DevCfg& c, uint16_t* ou
 
 // Initial traffic of a fresh episode (EpisodeMap scans pgtg/map.py:31-42 and
 // _create_initial_traffic pgtg/environment.py:830-879), run by k_traffic for the envs k_env reset.
-// `g` (1..4) adjacent lanes of a wave share one env (`sub` 0..g-1): lane 0 runs the serial parts
+// `g` (1..kMaxGroup) adjacent lanes of a wave share one env (`sub` 0..g-1): lane 0 runs the serial parts
 // (Floyd's choice, the shuffle, the per-car draws in id order); the sweep and the square lookup of
 // every chosen index, which have no RNG and no order, are split over the group.  `rs` is the env's
 // LDS reset scratch: Floyd's output [0, 2*cap) (then the chosen square codes), its seen set, the
@@ -1176,13 +1167,12 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
   }
   const int q0 = (int)(threadIdx.x & 63u) - sub;
   int np = 0, nsp = 0, tot_np = 0, tot_nsp = 0;
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int a = __shfl(cnp, q0 + (j < g ? j : 0)), b = __shfl(cnsp, q0 + (j < g ? j : 0));
+  for (int j = 0; j < g; j++) {  // (g is wave-uniform: every lane runs every shuffle)
+    const int a = __shfl(cnp, q0 + j), b = __shfl(cnsp, q0 + j);
     np += j < sub ? a : 0;
     nsp += j < sub ? b : 0;
-    tot_np += j < g ? a : 0;
-    tot_nsp += j < g ? b : 0;
+    tot_np += a;
+    tot_nsp += b;
   }
   uint32_t* colm = c.rs_cm_off ? reinterpret_cast<uint32_t*>(rs + c.rs_cm_off) : nullptr;
   for (int x = xa; x < xb; x++) {
@@ -3052,7 +3042,9 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
   if (rounds == 0) return;
   const uint32_t e = (n + W * rounds - 1) / (W * rounds);  // envs per wave and round, <= cap_w
   if ((uint64_t)blockIdx.x * (kBlock / 64) * e >= n) return;  // whole workgroup idle
-  const int g = e <= 16 ? 4 : (e <= 21 ? 3 : (e <= 32 ? 2 : 1));
+  // lanes per env: all a wave has for its e envs (<= kMaxGroup: the per-lane stretches of the sweep,
+  // the draws and the lookups stop paying once they are a few items long)
+  const int g = min(kMaxGroup, 64 / (int)e);
   const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
   const int slot = lane / g, sub = lane - slot * g;
   stage_tables(gtab, (int)sizeof(Tables));

@@ -1,7 +1,7 @@
 """k_traffic's launch shapes against the CPU oracle: the work list is levelled over the grid's waves
-(`e` envs per wave, in rounds beyond the LDS capacity `cap`) and each env gets 4, 3 or 2 lanes by `e`
+(`e` envs per wave, in rounds beyond the LDS capacity `cap`) and each env gets min(16, 64 / e) lanes
 (pgtg_env.hip k_traffic / traffic_reset).  The launch-shape overrides tune_kt_grid / tune_kt_cap force every
-shape with small batches: quads, triples, pairs, one env per wave in many rounds.  The per-car draws
+shape with small batches: 16, 12, 8, 4, 3 and 2 lanes per env, one env per wave in many rounds.  The per-car draws
 of the initial traffic run lane-parallel (cars_group: each lane jumps the env's car stream to its
 cars); tune_kt_serial forces the one-lane loop that a Lemire rejection falls back to."""
 
@@ -21,14 +21,18 @@ SHAPES = {
     "quads_e16": (512, 8, None, (5, 5)),     # e = 16 -> 4 lanes per env
     "triples_e20": (640, 8, None, (5, 5)),   # e = 20 -> 3 lanes
     "pairs_e25": (800, 8, None, (5, 5)),     # e = 25 -> 2 lanes
-    "rounds_cap1": (96, 4, 1, (5, 5)),       # e = 1, six rounds per wave
-    "rounds_cap5": (700, 4, 5, (5, 5)),      # e = 5 in nine rounds of the 16 waves, 4 lanes per env
+    "g16_e3": (96, 8, None, (5, 5)),         # e = 3 -> 16 lanes per env (the steady configs[2] shape)
+    "g8_e8": (256, 8, None, (5, 5)),         # e = 8 -> 8 lanes
+    "g12_e5": (160, 8, None, (5, 5)),        # e = 5 -> 12 lanes (a group that is no power of two)
+    "rounds_cap1": (96, 4, 1, (5, 5)),       # e = 1, six rounds per wave, 16 lanes per env
+    "rounds_cap5": (700, 4, 5, (5, 5)),      # e = 5 in nine rounds of the 16 waves, 12 lanes per env
     # more than seven tile rows: the lookup's per-tile row search instead of the column row masks
     "tall_map": (256, 8, None, (2, 9)),
     "wide_map": (256, 8, None, (9, 2)),
     # the per-car draws on one lane per env (the rejection fallback of cars_group)
     "serial_quads_e16": (512, 8, None, (5, 5), {"kt_serial": 1}),
     "serial_pairs_e25": (800, 8, None, (5, 5), {"kt_serial": 1}),
+    "serial_g16_e3": (96, 8, None, (5, 5), {"kt_serial": 1}),
 }
 
 
