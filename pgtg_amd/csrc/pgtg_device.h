@@ -101,9 +101,12 @@ struct DevCfg {
   double ind_reward[kMaxTiles + 1];
 };
 
-// Lane-indexed constant tables, copied once per workgroup into LDS (sT in pgtg_env.hip): the
-// 81-bit tile masks, the graph-theory edge order, border candidates and per-path-length rewards.
-struct Tables {
+// Lane-indexed constant tables, copied once per workgroup into LDS (pgtg_env.hip): the head (sT:
+// 81-bit tile masks, the graph-theory edge order, border candidates, per-path-length rewards) that
+// every step kernel reads, and the tail (sTX: lane, traffic, rule and driver tables) that only the
+// traffic and lane-channel paths read.  Two LDS objects, so that a kernel that never references the
+// tail (k_envq without lane channels) is not allocated its 10 KB.
+struct TablesHead {
   uint32_t wall[16][3];     // kTileWall
   uint32_t seg[4][3];       // kExitSeg
   uint32_t obst[14][3];     // kObstMask
@@ -117,6 +120,8 @@ struct Tables {
   // build different channels of one env's image (a per-lane index into the DevCfg block would be a
   // dependent global load per channel)
   uint8_t chan[PGTG_MAX_CHANNELS];
+};
+struct TablesTail {
   uint32_t lanes[16][81];   // kLanes (copied only when traffic or lane/spawner channels need it)
   // traffic tables (copied with lanes): lane-square slot per square (255 = none), square per slot,
   // per-column masks (bit ly) of lane squares, lane-data spawners and the four "all" lanes
@@ -133,6 +138,11 @@ struct Tables {
   uint64_t beh_t[5][5];    // [BEH_*][profile] 53-bit thresholds
   int32_t beh_mf[5], beh_pt[5];  // min_following_distance, floor(patience_level * 10)
 };
+// the global copy: head then tail, no padding between (asserted below)
+struct Tables : TablesHead, TablesTail {};
+constexpr size_t kTabHead = sizeof(TablesHead);  // byte offset of the tail in Tables
+static_assert(sizeof(TablesHead) % 16 == 0 && sizeof(TablesHead) % alignof(TablesTail) == 0, "tail offset");
+static_assert(sizeof(Tables) == sizeof(TablesHead) + sizeof(TablesTail), "Tables = head | tail");
 
 // one PCG64 stream, SoA over envs
 struct DevStream {

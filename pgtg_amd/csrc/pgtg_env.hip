@@ -39,14 +39,15 @@ namespace hs {
 #undef PGTG_TBL_QUAL
 }  // namespace hs
 
-__shared__ __attribute__((aligned(16))) Tables sT;  // per-workgroup LDS copy of the lane-indexed tables
+__shared__ __attribute__((aligned(16))) TablesHead sT;  // per-workgroup LDS copy of the tables' head
+__shared__ __attribute__((aligned(16))) TablesTail sTX;  // and of the tail (kernels that reference it)
 
-// Copy the first `bytes` of the tables into sT: all of a thread's 16-byte loads are issued before
-// the first LDS store (one memory latency instead of one per word).
-__device__ __forceinline__ void stage_tables(const Tables* __restrict__ gtab, int bytes) {
+// Copy `bytes` of a table into LDS: all of a thread's 16-byte loads are issued before the first
+// LDS store (one memory latency instead of one per word).
+__device__ __forceinline__ void stage_bytes(const void* __restrict__ gsrc, void* ldst, int bytes) {
   const int n4 = bytes >> 4, tid = (int)threadIdx.x;
-  const uint4* src = reinterpret_cast<const uint4*>(gtab);
-  uint4* dst = reinterpret_cast<uint4*>(&sT);
+  const uint4* src = reinterpret_cast<const uint4*>(gsrc);
+  uint4* dst = reinterpret_cast<uint4*>(ldst);
   uint4 r[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) r[j] = src[tid + j * kBlock < n4 ? tid + j * kBlock : 0];  // unconditional: registers, not scratch
@@ -55,7 +56,12 @@ __device__ __forceinline__ void stage_tables(const Tables* __restrict__ gtab, in
     if (tid + j * kBlock < n4) dst[tid + j * kBlock] = r[j];
   for (int k = tid + 4 * kBlock; k < n4; k += kBlock) dst[k] = src[k];
   for (int k = n4 * 4 + tid; k < bytes / 4; k += kBlock)
-    reinterpret_cast<uint32_t*>(&sT)[k] = reinterpret_cast<const uint32_t*>(gtab)[k];
+    reinterpret_cast<uint32_t*>(ldst)[k] = reinterpret_cast<const uint32_t*>(gsrc)[k];
+}
+// The head into sT; the tail into sTX when `tail` (a kernel whose code references sTX).
+__device__ __forceinline__ void stage_tables(const Tables* __restrict__ gtab, bool tail) {
+  stage_bytes(gtab, &sT, (int)sizeof(TablesHead));
+  if (tail) stage_bytes(reinterpret_cast<const uint8_t*>(gtab) + kTabHead, &sTX, (int)sizeof(TablesTail));
 }
 
 // Workgroup barrier for LDS data only: unlike __syncthreads() it does not wait for the waves'
@@ -227,7 +233,7 @@ __device__ __forceinline__ uint32_t square_lanes(const DevCfg& c, const Plan& pl
   int tx = x / kTile, ty = y / kTile;
   int lx = x - tx * kTile, ly = y - ty * kTile;
   uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
-  return ex ? sT.lanes[ex][lx * 9 + ly] : 0u;
+  return ex ? sTX.lanes[ex][lx * 9 + ly] : 0u;
 }
 __device__ __forceinline__ bool square_spawner(const DevCfg& c, const Plan& pl, int x, int y) {
   int tx = x / kTile, ty = y / kTile;
@@ -236,7 +242,7 @@ __device__ __forceinline__ bool square_spawner(const DevCfg& c, const Plan& pl, 
   if (!ex) return false;
   int sq = lx * 9 + ly;
   if (bit81(sT.spawner[ex], sq)) return true;
-  uint32_t l = sT.lanes[ex][sq];
+  uint32_t l = sTX.lanes[ex][sq];
   return (tx == 0 && (l >> 31 & 1u)) || (tx == c.tw - 1 && (l >> 30 & 1u)) || (ty == 0 && (l >> 29 & 1u)) ||
          (ty == c.th - 1 && (l >> 28 & 1u));
 }
@@ -256,7 +262,7 @@ __device__ __forceinline__ int lane_slot_tw(int tw, const Plan& pl, int x, int y
   int lx = x - tx * kTile, ly = y - ty * kTile;
   int t = ty * tw + tx;
   uint32_t ex = plan_exits(pl[t]);
-  const int li_raw = sT.li[ex][lx * 9 + ly];
+  const int li_raw = sTX.li[ex][lx * 9 + ly];
   const int li = ex ? li_raw : 255;
   return li == 255 ? -1 : t * 32 + li;
 }
@@ -343,11 +349,16 @@ constexpr uint32_t kCarEmpty = 1u << 31;  // w0 of a slot without a car
 // One env's car slots (DevState::car_w0 layout: slot k of env i at k * n + i) through per-lane
 // pointers at the env's slot 0: the three array bases stay in VGPRs instead of being re-read from
 // spilled scalar registers at every access of the car loops.
+// Global-address-space words: the slot pointers are pinned in VGPRs by the asm below, which hides
+// where they came from, and a generic pointer compiles to flat loads and stores -- and a flat access
+// counts on the LDS counter too, so every LDS wait of the car loop would also wait for the next
+// slot's HBM prefetch.
+typedef __attribute__((address_space(1))) uint32_t gu32;
 struct CarSlots {
-  uint32_t *w0, *w1, *id;
+  gu32 *w0, *w1, *id;
   uint64_t n;  // stride between slots (= number of envs)
   __device__ __forceinline__ CarSlots(const DevState& S, uint64_t i)
-      : w0(S.car_w0 + i), w1(S.car_w1 + i), id(S.car_id + i), n(S.n) {
+      : w0((gu32*)(S.car_w0 + i)), w1((gu32*)(S.car_w1 + i)), id((gu32*)(S.car_id + i)), n(S.n) {
     __asm__ volatile("" : "+v"(w0), "+v"(w1), "+v"(id));
   }
   __device__ __forceinline__ uint64_t at(int k) const { return (uint64_t)k * n; }
@@ -857,11 +868,11 @@ struct TrafState {
 // border rule of pgtg/parser.py:120-148 ("car_lane all right" on the west border, ...)
 __device__ __forceinline__ uint32_t spawner_colmask(const DevCfg& c, uint32_t ex, int tx, int ty, int lx) {
   if (!ex) return 0u;
-  uint32_t m = sT.spcol[ex][lx];
-  if (tx == 0) m |= sT.allcol[ex][3][lx];
-  if (tx == c.tw - 1) m |= sT.allcol[ex][2][lx];
-  if (ty == 0) m |= sT.allcol[ex][1][lx];
-  if (ty == c.th - 1) m |= sT.allcol[ex][0][lx];
+  uint32_t m = sTX.spcol[ex][lx];
+  if (tx == 0) m |= sTX.allcol[ex][3][lx];
+  if (tx == c.tw - 1) m |= sTX.allcol[ex][2][lx];
+  if (ty == 0) m |= sTX.allcol[ex][1][lx];
+  if (ty == c.th - 1) m |= sTX.allcol[ex][0][lx];
   return m;
 }
 
@@ -887,7 +898,7 @@ __device__ __forceinline__ CarSquare car_square(const DevCfg& c, const Plan& pl,
   const int tx = (int)((uint32_t)q.x / (uint32_t)kTile), ty = (int)((uint32_t)q.y / (uint32_t)kTile);
   q.tile = ty * c.tw + tx;
   q.sq = (q.x - tx * kTile) * 9 + (q.y - ty * kTile);
-  q.rl = sT.lanes[plan_exits(pl[q.tile])][q.sq] & 0x0fffffffu;
+  q.rl = sTX.lanes[plan_exits(pl[q.tile])][q.sq] & 0x0fffffffu;
   q.nr = __popc(q.rl);
   return q;
 }
@@ -910,7 +921,7 @@ __device__ __forceinline__ void car_squares(const DevCfg& c, const Plan& pl, con
   }
 #pragma unroll
   for (int u = 0; u < U; u++) {
-    q[u].rl = sT.lanes[plan_exits(p[u])][q[u].sq] & 0x0fffffffu;
+    q[u].rl = sTX.lanes[plan_exits(p[u])][q[u].sq] & 0x0fffffffu;
     q[u].nr = __popc(q[u].rl);
   }
 }
@@ -936,7 +947,7 @@ __device__ __forceinline__ int cars_serial(const DevCfg& c, const CarSlots& cs, 
     const uint64_t u = ahead_draw(ca, false, 0u);
     const int prof = profile_of(pcdf, u);
     const uint32_t rk = q.nr > 1u ? (uint32_t)ahead_draw(ca, true, q.nr) : 0u;
-    store_new_car(cs, a_m, q, sT.lane_route[kth_bit(q.rl, (int)rk)], prof, m);
+    store_new_car(cs, a_m, q, sTX.lane_route[kth_bit(q.rl, (int)rk)], prof, m);
     a_m += cs.n;
   }
   cr = ca.g;
@@ -1038,7 +1049,7 @@ __device__ __forceinline__ int cars_group(const DevCfg& c, const CarSlots& cs, c
       }
       int route[kCarChunk];
 #pragma unroll
-      for (int u = 0; u < kCarChunk; u++) route[u] = sT.lane_route[lr[u]];
+      for (int u = 0; u < kCarChunk; u++) route[u] = sTX.lane_route[lr[u]];
 #pragma unroll
       for (int u = 0; u < kCarChunk; u++) {
         if (m + u < m1) store_new_car(cs, a_m, q[u], route[u], prof[u], m + u);
@@ -1161,7 +1172,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
     const int tx = x / kTile, lx = x - tx * kTile;
     for (int ty = 0; ty < c.th; ty++) {
       const uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
-      cnp += __popc(sT.lanecol[ex][lx]);  // row 0 (no exits) is empty
+      cnp += __popc(sTX.lanecol[ex][lx]);  // row 0 (no exits) is empty
       cnsp += __popc(spawner_colmask(c, ex, tx, ty, lx));
     }
   }
@@ -1181,7 +1192,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
     uint64_t cm = 0;
     for (int ty = 0; ty < c.th; ty++) {
       const uint32_t ex = plan_exits(pl[ty * c.tw + tx]);
-      const uint32_t lc = sT.lanecol[ex][lx];
+      const uint32_t lc = sTX.lanecol[ex][lx];
       np += __popc(lc);
       cm |= (uint64_t)lc << (9 * (ty & 7));
       uint32_t m = spawner_colmask(c, ex, tx, ty, lx);
@@ -1307,7 +1318,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
           int ty_f = 0, rr_f = 0, r = rr[u];
           uint32_t msk_f = 0;
           for (int ty = 0; ty < th; ty++) {
-            const uint32_t msk = sT.lanecol[plan_exits(pl[ty * tw + txu])][lx];
+            const uint32_t msk = sTX.lanecol[plan_exits(pl[ty * tw + txu])][lx];
             const int cnt = __popc(msk);
             if (r >= 0 && r < cnt) {
               ty_f = ty;
@@ -1511,7 +1522,7 @@ struct BitSink {
 // the window's squares row-major over x, then y.
 // Channels [ch_lo, ch_hi) only (default all) when the lanes of a group share one env's image (the
 // group's sinks merge at their shared words); `head`: also the next-subgoal direction.
-template <bool TR, bool BIG>
+template <bool TR, bool BIG, bool LC = true>  // LC: lane / spawner channels possible (they read sTX)
 __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
                                           uint32_t* img, uint32_t bit0, ObsInfo& oi, const uint8_t* occ,
                                           int ch_lo = 0, int ch_hi = -1, bool head = true, bool lane_codes = false) {
@@ -1552,7 +1563,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
         while (nz) {
           const int sl = q * 8 + ((__ffs((int)nz) - 1) >> 2);
           nz &= nz - 1u;
-          const int sq = sT.slot_sq[ex][sl];
+          const int sq = sTX.slot_sq[ex][sl];
           CR[sq >> 5] |= 1u << (sq & 31);
         }
       }
@@ -1626,8 +1637,8 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
             bool sp = false;
             if (inside(c, x, y)) {
               f = square_flags<BIG>(c, pl, v, x, y);
-              if (code == PGTG_CH_SPAWNER) sp = square_spawner(c, pl, x, y);
-              if (code >= PGTG_CH_LANE0) lanes = square_lanes(c, pl, x, y);
+              if (LC && code == PGTG_CH_SPAWNER) sp = square_spawner(c, pl, x, y);
+              if (LC && code >= PGTG_CH_LANE0) lanes = square_lanes(c, pl, x, y);
             } else {
               f = c.sliding ? SQ_WALL : 0u;  // get_map_cutout fill {"wall"} for sliding windows
             }
@@ -1759,17 +1770,17 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       const uint32_t p0 = pl[t0];
       const uint32_t pn0 = pl[ok0 ? nt0 : t0], pn1 = pl[ok1 ? nt1 : t0];
       const uint32_t pn2 = pl[ok2 ? nt2 : t0], pn3 = pl[ok3 ? nt3 : t0];
-      const uint32_t rtl = *reinterpret_cast<const uint32_t*>(sT.route_type_lane[route]);
+      const uint32_t rtl = *reinterpret_cast<const uint32_t*>(sTX.route_type_lane[route]);
       // this car's behaviour thresholds (environment.py:64-109), read up front
-      const uint64_t th_delay = sT.beh_t[BEH_DELAY][prof], th_speed = sT.beh_t[BEH_SPEED][prof];
-      const uint64_t th_yellow = sT.beh_t[BEH_YELLOW][prof], th_red = sT.beh_t[BEH_RED][prof];
-      const uint64_t th_go = sT.beh_t[BEH_GO][prof];
-      const int b_mf = sT.beh_mf[prof], b_pt = sT.beh_pt[prof];
+      const uint64_t th_delay = sTX.beh_t[BEH_DELAY][prof], th_speed = sTX.beh_t[BEH_SPEED][prof];
+      const uint64_t th_yellow = sTX.beh_t[BEH_YELLOW][prof], th_red = sTX.beh_t[BEH_RED][prof];
+      const uint64_t th_go = sTX.beh_t[BEH_GO][prof];
+      const int b_mf = sTX.beh_mf[prof], b_pt = sTX.beh_pt[prof];
       const uint32_t e0 = ok0 ? plan_exits(pn0) : 0u, e1 = ok1 ? plan_exits(pn1) : 0u;
       const uint32_t e2 = ok2 ? plan_exits(pn2) : 0u, e3 = ok3 ? plan_exits(pn3) : 0u;
-      const int s_old = t0 * 32 + sT.li[plan_exits(p0)][sq];
-      const uint32_t l0 = sT.lanes[e0][nq0], l1 = sT.lanes[e1][nq1];  // row 0 (no exits) is empty
-      const uint32_t l2 = sT.lanes[e2][nq2], l3 = sT.lanes[e3][nq3];
+      const int s_old = t0 * 32 + sTX.li[plan_exits(p0)][sq];
+      const uint32_t l0 = sTX.lanes[e0][nq0], l1 = sTX.lanes[e1][nq1];  // row 0 (no exits) is empty
+      const uint32_t l2 = sTX.lanes[e2][nq2], l3 = sTX.lanes[e3][nq3];
       int dec = -1;
       bool dec_all = false;
 #pragma unroll
@@ -1791,7 +1802,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       const uint32_t wall_tg = bit81(sT.wall[ex_tg], dec < 0 ? sq : tg_q);
       const uint32_t obst_tg = bit81(sT.obst[min(plan_omask(p_tg), (uint32_t)PGTG_N_OBST_MASKS - 1u)], dec < 0 ? sq : tg_q);
       const bool tl = plan_otype(p_tg) == 4u && !wall_tg && obst_tg;
-      const int li_tg = sT.li[ex_tg][tg_q];
+      const int li_tg = sTX.li[ex_tg][tg_q];
       const int s_tg = dec < 0 ? s_old : tg_t * 32 + li_tg;
       const int occ_raw = occ_get(occ, s_tg);
       const int occ_tg = dec < 0 ? 0 : occ_raw;
@@ -1831,7 +1842,10 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
         // _spawn_new_car: choice(car_spawners) -> sorted routes -> profile -> route
         int sx = 0, sy = 0;
         if (nsp > 0) {
-          const uint32_t code = r3 < (uint64_t)kSpCache ? sp[r3] : S.spawners[r3 * S.n + i];
+          // (two loads, not one through a selected pointer: that would be a flat load, whose wait
+          // covers the LDS counter and the slot prefetch)
+          uint32_t code = sp[r3 < (uint64_t)kSpCache ? r3 : 0];
+          if (r3 >= (uint64_t)kSpCache) code = ((const __attribute__((address_space(1))) uint16_t*)S.spawners)[r3 * S.n + i];
           sx = (int)(code & 255u);
           sy = (int)(code >> 8);
         }
@@ -1840,7 +1854,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
         const int nprof = profile_of(pcdf, r4);
         if (nr == 0) return PGTG_E_MAP;
         const uint32_t r5 = nr > 1u ? (uint32_t)pcg_draw(ca, true, nr) : 0u;
-        const int nroute = sT.lane_route[kth_bit(rl, (int)r5)];
+        const int nroute = sTX.lane_route[kth_bit(rl, (int)r5)];
         if (!pack) cs.w0[aw] = kCarEmpty;
         cs.w0[an] = (uint32_t)sx | (uint32_t)sy << 8 | (uint32_t)nroute << 16 | (uint32_t)nprof << 21;
         cs.w1[an] = 0u;
@@ -1855,7 +1869,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
           hist[nroute]++;
         }
       } else {
-        if (kind == 1) route = sT.lane_route[kth_bit(tg_ln & 0x0fffffffu, (int)r3)];
+        if (kind == 1) route = sTX.lane_route[kth_bit(tg_ln & 0x0fffffffu, (int)r3)];
         int nx = x, ny = y, s_cur = s_old;
         if (leaves) {
           nx = x + (dk == 2 ? -1 : (dk == 3 ? 1 : 0));
@@ -1930,7 +1944,7 @@ __device__ __forceinline__ uint32_t braking_decide(const DevCfg& c, const DevSta
     if (!((q.cand >> r) & 1u)) continue;
     if (q.n_in < c.rules[r].min_traffic) continue;
     int match = 0;
-    for (int k = 0; k < 20; k++) match += hist[k] * (int)sT.rule_w[r][dir][k];
+    for (int k = 0; k < 20; k++) match += hist[k] * (int)sTX.rule_w[r][dir][k];
     if (match >= c.rules[r].min_matching_traffic) trig |= 1u << r;
   }
   return trig;
@@ -2306,9 +2320,9 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.stream_words = img_words(l.sub_envs, l.seg_bits);
   l.spread = c.need_car ? 1 : 0;
   l.compact = 1;
-  // map queue: random maps without traffic or braking rules (k_envq), a whole-workgroup observation
-  // image and at least one wave without env slots
-  l.queue = !c.need_car && c.n_rules == 0 && !c.fixed_map && envs <= kBlock - 64 && l.sub_envs >= envs;
+  // map queue: random maps without traffic, braking rules or lane channels (k_envq), a whole-workgroup
+  // observation image and at least one wave without env slots
+  l.queue = !c.need_car && c.n_rules == 0 && !c.fixed_map && !c.generic_channels && envs <= kBlock - 64 && l.sub_envs >= envs;
   l.stagger = 0;
   l.stagger_wgs = 0;
 #ifdef PGTG_TUNING  // A/B and diagnostic builds only: the product library reads no environment
@@ -2412,7 +2426,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   // the traffic-reset list of the next launch starts empty (its previous consumer has finished)
   if ((TR && c.need_car) && mode != MODE_OBSERVE && blockIdx.x == 0 && tid == 0) S.tr_count[tr_slot ^ 1u] = 0u;
   // stage the lane-indexed tables (kLanes only when a pass needs it)
-  stage_tables(gtab, (int)(c.generic_channels || (TR && c.need_car) ? sizeof(Tables) : offsetof(Tables, lanes)));
+  stage_tables(gtab, c.generic_channels || (TR && c.need_car));
   const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
   const int nb = (int)min((uint64_t)L.envs, S.n - env0);
   // env slots: E/4 per wave when a workgroup holds fewer than 256 envs, so that all four SIMDs
@@ -2752,7 +2766,7 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
     const int C = c.n_channels;
     extern __shared__ uint32_t lds[];
     const Plan pl{reinterpret_cast<uint16_t*>(lds + e * L.plan_stride_dw)};
-    build_obs<false, BIG>(c, S, pl, ve, st, (uint32_t)e * (uint32_t)c.obs_bytes, oi, nullptr, sub * C / G,
+    build_obs<false, BIG, false>(c, S, pl, ve, st, (uint32_t)e * (uint32_t)c.obs_bytes, oi, nullptr, sub * C / G,
                      (sub + 1) * C / G, sub == 0, true);
     STAMP(post ? 11 : 18);
     return;
@@ -2761,7 +2775,7 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
     extern __shared__ uint32_t lds[];
     const int slot = (int)threadIdx.x;
     const Plan pl{reinterpret_cast<uint16_t*>(lds + slot * L.plan_stride_dw)};
-    build_obs<false, BIG>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
+    build_obs<false, BIG, false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
   }
 }
 
@@ -2774,7 +2788,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint64_t t_start = stagger_start(L, S);
   STAMP(0);
-  stage_tables(gtab, (int)(c.generic_channels ? sizeof(Tables) : offsetof(Tables, lanes)));
+  stage_tables(gtab, false);  // (the map queue runs without lane channels: no sTX reference here)
   const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
   const int nb = (int)min((uint64_t)L.envs, S.n - env0);
   const int env_waves = (L.envs + 63) / 64, gen_wave = env_waves;
@@ -2992,7 +3006,7 @@ __global__ void __launch_bounds__(kBlock) k_gen_bench(const DevCfg* __restrict__
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
     uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
-    for (int k = threadIdx.x; k < (int)(offsetof(Tables, lanes) / 4); k += blockDim.x) dstt[k] = src[k];
+    for (int k = threadIdx.x; k < (int)(sizeof(TablesHead) / 4); k += blockDim.x) dstt[k] = src[k];
   }
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -3047,7 +3061,7 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
   const int g = min(kMaxGroup, 64 / (int)e);
   const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
   const int slot = lane / g, sub = lane - slot * g;
-  stage_tables(gtab, (int)sizeof(Tables));
+  stage_tables(gtab, true);
   __syncthreads();
   STAMP(25);
 #ifdef PGTG_STAMPS
@@ -3105,7 +3119,9 @@ __global__ void __launch_bounds__(kBlock) k_squares(const DevCfg* __restrict__ c
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab);
     uint32_t* dstt = reinterpret_cast<uint32_t*>(&sT);
-    for (int k = tid; k < (int)(sizeof(Tables) / 4); k += blockDim.x) dstt[k] = src[k];
+    for (int k = tid; k < (int)(sizeof(TablesHead) / 4); k += blockDim.x) dstt[k] = src[k];
+    uint32_t* dstx = reinterpret_cast<uint32_t*>(&sTX);
+    for (int k = tid; k < (int)(sizeof(TablesTail) / 4); k += blockDim.x) dstx[k] = src[kTabHead / 4 + k];
     for (int t = tid; t < c.nt; t += blockDim.x) plan_s[t] = S.plan[i * (uint64_t)c.plan_stride + t];
   }
   __syncthreads();
@@ -3578,7 +3594,7 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
   // episodes' maps (k_envq, the map queue: 1 048 576 5x5 envs 2.27 G vs 1.77 G env-steps/s), smaller
   // maps, fixed maps and rules a full workgroup of env lanes (262 144 3x3 envs: 2.50 G vs 2.07 G);
   // traffic 128 (LDS).
-  const bool queue_able = allow_queue && !c.need_car && c.n_rules == 0 && !c.fixed_map && c.nt >= 16;
+  const bool queue_able = allow_queue && !c.need_car && c.n_rules == 0 && !c.fixed_map && !c.generic_channels && c.nt >= 16;
   int envs = c.need_car ? 128
            : n_envs <= (uint64_t)8 * 1024 ? 16
            : n_envs <= (uint64_t)16 * 1024 ? 32
@@ -3657,7 +3673,7 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
   // map queue (k_envq): recheck after the adjustments above, place the helper scratch
   h->L.queue = h->L.queue && allow_queue && h->L.sub_envs >= h->L.envs && h->L.envs <= kBlock - 64;
   lds_tail(h->L, c);
-  if (h->L.queue && lds_bytes(h->L) + sizeof(Tables) > 40 * 1024) {  // keep 4 workgroups per CU
+  if (h->L.queue && lds_bytes(h->L) + kTabHead > 40 * 1024) {  // keep 4 workgroups per CU
     h->L.queue = 0;
     lds_tail(h->L, c);
   }
@@ -4144,7 +4160,7 @@ int pgtg_set_rules(pgtg_handle* h, const PgtgRule* rules, int32_t n_rules) {
   uint8_t w[PGTG_MAX_RULES][6][20] = {};
   for (int k = 0; k < n_rules; k++) memcpy(w[k], rules[k].weight, sizeof w[k]);
   HIPCHK(h, hipMemcpy(h->dcfg, &c, sizeof(DevCfg), hipMemcpyHostToDevice));
-  HIPCHK(h, hipMemcpy(reinterpret_cast<uint8_t*>(h->dtab) + offsetof(Tables, rule_w), w, sizeof w, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(reinterpret_cast<uint8_t*>(h->dtab) + kTabHead + offsetof(TablesTail, rule_w), w, sizeof w, hipMemcpyHostToDevice));
   return PGTG_OK;
 }
 
@@ -4504,7 +4520,7 @@ int pgtg_occupancy(const pgtg_handle* h, int32_t* step_blocks_per_cu) {
 int pgtg_launch_info(const pgtg_handle* h, int32_t* envs_per_block, int32_t* lds_bytes) {
   if (!h) return PGTG_E_INVALID;
   if (envs_per_block) *envs_per_block = h->L.envs;
-  if (lds_bytes) *lds_bytes = (int32_t)(h->lds + sizeof(Tables));
+  if (lds_bytes) *lds_bytes = (int32_t)(h->lds + (h->L.queue ? kTabHead : sizeof(Tables)));  // + the static table copy
   return PGTG_OK;
 }
 const char* pgtg_last_error(const pgtg_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
