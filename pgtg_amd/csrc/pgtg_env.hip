@@ -2748,6 +2748,7 @@ __device__ __forceinline__ void sub_barrier(uint32_t* ctr, uint32_t target) {
 template <bool BIG>
 __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, const EnvView& v, bool want,
                                           uint32_t* st, ObsInfo& oi, const Lds& L, int wave, int lane, bool post = true) {
+  const int vtid = wave * 64 + lane;
   const int E = L.envs;
   if (E <= 32) {
     if (wave != 0) return;
@@ -2773,7 +2774,7 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
   }
   if (want) {
     extern __shared__ uint32_t lds[];
-    const int slot = (int)threadIdx.x;
+    const int slot = vtid;
     const Plan pl{reinterpret_cast<uint16_t*>(lds + slot * L.plan_stride_dw)};
     build_obs<false, BIG, false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
   }
