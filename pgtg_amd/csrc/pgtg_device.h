@@ -167,11 +167,16 @@ struct DevState {
   // coalesced access.  w0 = x | y<<8 | route<<16 | profile<<21 | delay<<24 (bit 31: empty slot, a
   // despawned car), w1 = patience counter, id = car id.  Survivors are rewritten in place, respawns
   // appended behind the tail, the slots compacted when a tick's respawns could overrun them.
-  // traf[n] = {n_cars | n_spawners<<16, next_id, tail (slots in use), 0}
+  // traf[n] = {n_cars | n_spawners<<16, next_id, tail (slots in use), occ_valid}
+  // occ: the 4-bit lane-square occupancy counters (nt * 4 words per env, slot-major [word][n]) as the
+  // last launch left them; traf.w == 1 when they are exact for the env's current cars (written by
+  // k_traffic for fresh traffic, by k_env after a step whose counters never saturated), else k_env
+  // rebuilds them from the car slots
   uint32_t* car_w0;
   uint32_t* car_w1;
   uint32_t* car_id;
   uint4* traf;
+  uint32_t* occ;          // [nt * 4][n] or null
   uint16_t* spawners;     // [max_spawners][n] square codes x | y<<8, x-major order
   uint32_t* tr_list;      // [n] envs k_env reset this launch (k_traffic's work list)
   uint32_t* tr_count;     // [2] list lengths, alternating launches

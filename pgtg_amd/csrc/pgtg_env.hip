@@ -1349,6 +1349,26 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
   return 0;
 }
 
+// The occupancy counters of a fresh env's k cars (square codes x | y << 8 in out[0, k), one car per
+// square: no counter overflows) for k_env, which loads them instead of rebuilding them from the car
+// slots.  The g lanes of the env's group count into `cnt` (the reset scratch from rs_jj_off, free
+// once the cars exist) with LDS adds and store the nt * 4 words to S.occ.
+__device__ __forceinline__ void store_initial_counters(const DevCfg& c, const DevState& S, uint64_t i, const Plan& pl,
+                                                       uint8_t* rs, int k, int sub, int g) {
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(rs + c.rs_jj_off);
+  const uint16_t* out = reinterpret_cast<const uint16_t*>(rs);
+  const int nw = c.nt * 4;
+  for (int w = sub; w < nw; w += g) cnt[w] = 0u;
+  wave_lds_sync();
+  for (int m = k * sub / g; m < k * (sub + 1) / g; m++) {
+    const uint32_t code = out[m];
+    const int s = lane_slot(c, pl, (int)(code & 255u), (int)(code >> 8));
+    if (s >= 0) __hip_atomic_fetch_add(cnt + (s >> 3), 1u << ((s & 7) << 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
+  wave_lds_sync();
+  for (int w = sub; w < nw; w += g) S.occ[(uint64_t)w * S.n + i] = cnt[w];
+}
+
 // The full per-env reset.  `key` = spawn counter (5 children per episode).  Returns 0 or -code.
 template <bool TR, bool BIG>
 __device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uint64_t i, EnvView& v, uint16_t* plan,
@@ -2455,6 +2475,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   EnvView v{};
   TrafState ts{0, 0, 0, 0};
   bool occ_sat = false;  // a 4-bit occupancy counter saturated this launch (exact recounts from then on)
+  bool occ_valid = false;  // the persisted counters of this env are exact (traf.w)
   int err = 0;
   int act = 0;
   if (live) {
@@ -2466,12 +2487,25 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       ts.n_spawners = tr4.x >> 16;
       ts.next_id = tr4.y;
       ts.tail = tr4.z;
+      occ_valid = tr4.w == 1u;
     }
     stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, L.plan_stride_dw);
   }
   for (int k = tid; k < L.lm_words; k += kBlock) lm[k] = 0u;
   lds_barrier();  // sT ready
-  if (live && (TR && c.need_car)) {
+  if (live && (TR && c.need_car) && occ_valid) {
+    // the counters the last launch (or k_traffic) left: one coalesced row per counter word
+    const int nw = c.nt * 4;
+    for (int w0 = 0; w0 < nw; w0 += 16) {
+      uint32_t r[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) r[u] = S.occ[(uint64_t)min(w0 + u, nw - 1) * S.n + i];
+#pragma unroll
+      for (int u = 0; u < 16; u++)
+        if (w0 + u < nw) traf_w[w0 + u] = r[u];
+    }
+  }
+  if (live && (TR && c.need_car) && !occ_valid) {
     // occupancy counters from the current car positions (one coalesced slot row per slot index, 16
     // loads in flight per lane, the next 16 requested before the counters of the current ones are
     // updated so that their HBM latency overlaps the LDS work)
@@ -2500,6 +2534,8 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
         }
       }
     }
+  }
+  if (live && (TR && c.need_car)) {
     // the head of the spawner list (respawn positions) into LDS
     const int nsp = min((int)ts.n_spawners, kSpCache);
     for (int k0 = 0; k0 < nsp; k0 += 8) {
@@ -2517,6 +2553,11 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     if (mode == MODE_STEP) {
       StepResult res{0.0, 0.0, 0u};
       if (!err) err = env_step<TR, BIG>(c, S, i, v, pl, act, res, occ, occ_sat, sp_l, ts, hist);
+      if ((TR && c.need_car) && !occ_sat) {  // the counters after the car pass, for the next launch
+        const int nw = c.nt * 4;
+        for (int w = 0; w < nw; w++) S.occ[(uint64_t)w * S.n + i] = traf_w[w];
+      }
+      occ_valid = (TR && c.need_car) && !occ_sat && err == 0;
       const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
       // BIG maps keep the used subgoals in the plan: the row goes back to HBM unless the env resets now
       if (BIG && res.plan_dirty && !(done && c.autoreset && err == 0)) store_plan_row(c, S, i, plan_w, L.plan_stride_dw);
@@ -2633,7 +2674,9 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (live) {
     if (mode != MODE_OBSERVE) {
       rec_store(S.rec, i, v);
-      if ((TR && c.need_car)) S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.tail, 0u);
+      // (a reset env's counters come from k_traffic with its fresh cars; until then invalid)
+      if ((TR && c.need_car))
+        S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.tail, occ_valid && !reset_now ? 1u : 0u);
     }
     if (mode != MODE_OBSERVE || err) S.err[i] = (uint8_t)(-err);
     if (S.qstate && reset_now) S.qstate[i] = 0;  // maps generated here: the queued ones are stale
@@ -3088,9 +3131,12 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
     TrafState ts{0, 0, 0, 0};
     uint32_t CR[3] = {0u, 0u, 0u};
     const int err = traffic_reset(c, S, i, pl, cr, rs, ts, at, CR, sub, g);
+    const int q0 = lane - sub;  // (traffic_reset's result is lane 0's)
+    const int err0 = __shfl(err, q0), k0 = __shfl((int)ts.n_cars, q0);
+    if (err0 == 0) store_initial_counters(c, S, i, pl, rs, k0, sub, g);
     if (sub == 0) {
       stream_store_state(S.car, i, cr);
-      S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.tail, 0u);
+      S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.tail, err == 0 ? 1u : 0u);
       if (err) S.err[i] = (uint8_t)(-err);
       if (c.obs_fast && c.traffic_ch >= 0 && out.obs) {
         // the tile window's traffic channel: k_env wrote it with no cars; set the car squares
@@ -3529,6 +3575,7 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
     c.rs_seen_off = c.rs_jj_off + ((2 * cap + 3) / 4) * 4;
     c.rs_pre_off = c.rs_seen_off + 4 * c.nt;
     c.rs_bytes = (c.rs_pre_off + 2 * (c.W + 1) + 3) / 4 * 4;
+    c.rs_bytes = std::max(c.rs_bytes, c.rs_jj_off + 16 * c.nt);  // store_initial_counters' words
     c.rs_cm_off = 0;
     if (c.th <= 7) {  // a column's spawnable squares as one 63-bit mask: the lookup's row search is one read
       c.rs_cm_off = c.rs_bytes;
@@ -3771,6 +3818,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     ALLOC(S.car_w1, (uint64_t)c.car_slots * n);
     ALLOC(S.car_id, (uint64_t)c.car_slots * n);
     ALLOC(S.traf, n);
+    ALLOC(S.occ, (uint64_t)c.nt * 4 * n);
     ALLOC(S.spawners, (uint64_t)c.max_spawners * n);
     ALLOC(S.tr_list, n);
     ALLOC(S.tr_count, 2);
@@ -4065,6 +4113,7 @@ static int host_write_cars(pgtg_handle* h, uint64_t env, uint4 t, const std::vec
   t.x = (t.x & 0xffff0000u) | (uint32_t)n;
   t.y = next_id;
   t.z = (uint32_t)n;
+  t.w = 0u;  // the persisted occupancy counters no longer match: the next launch rebuilds them
   HIPCHK(h, hipMemcpy(h->S.traf + env, &t, sizeof t, hipMemcpyHostToDevice));
   return 0;
 }
@@ -4253,6 +4302,7 @@ static std::vector<StateSection> state_sections(pgtg_handle* h) {
   add(32, S.car_w1, (uint64_t)c.car_slots * n * 4);
   add(33, S.car_id, (uint64_t)c.car_slots * n * 4);
   add(34, S.traf, n * sizeof(uint4));
+  add(36, S.occ, (uint64_t)c.nt * 4 * n * 4);
   add(35, S.spawners, (uint64_t)c.max_spawners * n * 2);
   add(40, S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw * 4);
   add(41, S.qstate, n);
