@@ -1545,7 +1545,8 @@ struct BitSink {
 template <bool TR, bool BIG, bool LC = true>  // LC: lane / spawner channels possible (they read sTX)
 __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
                                           uint32_t* img, uint32_t bit0, ObsInfo& oi, const uint8_t* occ,
-                                          int ch_lo = 0, int ch_hi = -1, bool head = true, bool lane_codes = false) {
+                                          int ch_lo = 0, int ch_hi = -1, bool head = true, bool lane_codes = false,
+                                          bool occ_tile_only = false) {  // occ: the agent tile's 16 bytes only
   const int WW = c.win * c.win;
   if (ch_hi < 0) ch_hi = c.n_channels;
   BitSink sink(img, bit0 + (uint32_t)(ch_lo * WW));
@@ -1575,7 +1576,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
     uint32_t ot = plan_otype(p);
     uint32_t CR[3] = {0, 0, 0};  // squares of this tile holding a car
     if ((TR && c.need_car) && occ && ex) {
-      const uint32_t* ow = reinterpret_cast<const uint32_t*>(occ + t * 16);  // the tile's 32 nibbles
+      const uint32_t* ow = reinterpret_cast<const uint32_t*>(occ + (occ_tile_only ? 0 : t * 16));  // the tile's 32 nibbles
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const uint32_t wv = ow[q];
@@ -2314,6 +2315,8 @@ struct Lds {
   int lm_words;        // terminal-observation line mask words (0: test the selection bytes)
   int stagger;         // first-round start offsets (stagger_start) on
   int stagger_wgs;     // workgroups resident in the first round (blocks per CU x CUs)
+  int img_in_traf;     // k_env with traffic: the whole workgroup's image in the (after the car pass dead)
+                       // traffic region; the agent tile's counters and the reset hand-over words in hist
 };
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
 constexpr uint64_t kStaggerMaxTicks = 20000;  // 200 us of 100 MHz wall clock: a bound, never reached
@@ -2345,6 +2348,7 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.queue = !c.need_car && c.n_rules == 0 && !c.fixed_map && !c.generic_channels && envs <= kBlock - 64 && l.sub_envs >= envs;
   l.stagger = 0;
   l.stagger_wgs = 0;
+  l.img_in_traf = 0;
 #ifdef PGTG_TUNING  // A/B and diagnostic builds only: the product library reads no environment
   if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);
   if (const char* e = getenv("PGTG_COMPACT")) l.compact = atoi(e);
@@ -2372,6 +2376,21 @@ __host__ inline void lds_tail(Lds& l, const DevCfg& c) {
 __host__ inline size_t lds_bytes(const Lds& l) {
   return (size_t)4 * ((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
          tail_bytes(l) + (l.queue ? (size_t)4 * kQueueLanes * l.plan_stride_dw : 0);
+}
+
+// Traffic launches with one-tile windows: once the car pass is over, the traffic region (occupancy
+// counters, spawner cache) is dead except for the 16 counter bytes of the agent's tile that the
+// traffic channel reads, so the whole workgroup's observation image goes there (one pass instead of
+// sub-batches) and hist (the braking histogram, dead after the step too) keeps those 16 bytes and the
+// reset hand-over words: hist = 4 counter words + 3 hand-over words.
+__host__ inline void lds_img_in_traf(Lds& l, const DevCfg& c) {
+  if (!c.need_car || !c.obs_fast || l.envs < 1) return;
+  if ((int64_t)img_words(l.envs, l.seg_bits) > (int64_t)l.envs * l.traf_dw) return;
+  l.img_in_traf = 1;
+  l.sub_envs = l.envs;
+  l.stream_words = 0;
+  l.hist_dw = 7;
+  lds_tail(l, c);
 }
 
 enum { MODE_STEP = 0, MODE_RESET_SEEDED = 1, MODE_RESET_UNSEEDED = 2, MODE_OBSERVE = 3 };
@@ -2460,12 +2479,15 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   uint32_t* plan_w = lds + my_slot * L.plan_stride_dw;
   uint32_t* traf_w = lds + L.envs * (L.plan_stride_dw + L.scratch_dw) + my_slot * L.traf_dw;
   uint32_t* hist_w = lds + L.envs * (L.plan_stride_dw + L.scratch_dw + L.traf_dw) + my_slot * L.hist_dw;
-  uint32_t* st = lds + L.envs * (L.plan_stride_dw + L.scratch_dw + L.traf_dw + L.hist_dw);
-  uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
+  const int env_dw = L.plan_stride_dw + L.scratch_dw + L.traf_dw + L.hist_dw;
+  uint32_t* st = (TR && L.img_in_traf) ? lds + L.envs * (L.plan_stride_dw + L.scratch_dw) : lds + L.envs * env_dw;
+  uint8_t* sel = reinterpret_cast<uint8_t*>(lds + L.envs * env_dw + L.stream_words);  // [kBlock]
   uint64_t* wmask = reinterpret_cast<uint64_t*>(sel + kBlock);     // [4] reset ballot per wave
   uint32_t* lm = L.lm_words ? reinterpret_cast<uint32_t*>(sel + kBlock + 32) : nullptr;  // terminal lines
-  const int xf_off = L.envs * L.plan_stride_dw + ((TR && c.need_car) ? L.envs * L.scratch_dw : 0);
-  const int xf_dw = (TR && c.need_car) ? L.traf_dw : L.scratch_dw;
+  const bool img_traf = TR && L.img_in_traf;
+  const int xf_off = img_traf ? L.envs * (L.plan_stride_dw + L.scratch_dw + L.traf_dw) + 4
+                   : L.envs * L.plan_stride_dw + ((TR && c.need_car) ? L.envs * L.scratch_dw : 0);
+  const int xf_dw = img_traf ? L.hist_dw : (TR && c.need_car) ? L.traf_dw : L.scratch_dw;
   uint32_t* xf = lds + xf_off + my_slot * xf_dw;  // reset hand-over words
   uint8_t* occ = reinterpret_cast<uint8_t*>(traf_w);
   uint16_t* sp_l = reinterpret_cast<uint16_t*>(occ + c.sp_cache_off);  // first spawners of the list
@@ -2575,6 +2597,18 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     }
   }
   if (has_slot) sel[slot] = my_sel;
+  // the images read the counters of the agent's tile only: with the image in the traffic region, those
+  // 16 bytes move to hist first (the barrier below orders this before any image store)
+  const uint8_t* occ_img = occ;
+  if (img_traf) {
+    if (live) {
+      const int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
+      const int t = (piy / kTile) * c.tw + pix / kTile;
+#pragma unroll
+      for (int q = 0; q < 4; q++) hist_w[q] = traf_w[t * 4 + q];
+    }
+    occ_img = hist;
+  }
   STAMP(2);
   const bool single = L.sub_envs >= nb;  // the whole workgroup's image fits: build once, rebuild resets
   const bool reset_now = my_sel != 0;
@@ -2609,7 +2643,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (single) {
     if (live && (my_sel != 2)) {
       ObsInfo oi;
-      build_obs<TR, BIG>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, occ);
+      build_obs<TR, BIG>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, occ_img, 0, -1, true, false, img_traf);
       write_small_outputs(c, out, i, v, oi, my_sel == 1);
     }
     if (L.compact && reset_now) xf[0] = v.spawn;  // after the terminal image read the counters
@@ -3694,6 +3728,8 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
   if (h->tune_obs_sub >= 1 && h->tune_obs_sub < h->L.sub_envs) {  // forced observation sub-batch
     h->L.sub_envs = h->tune_obs_sub;
     h->L.stream_words = img_words(h->tune_obs_sub, h->L.seg_bits);
+  } else {
+    lds_img_in_traf(h->L, c);
   }
   if (c.need_car) {
     // k_traffic: per-lane plan + reset scratch
