@@ -196,7 +196,8 @@ int pgtg_set_agent(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t v
 int pgtg_add_car(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_t route, int32_t profile, int32_t car_id);
 /* Whole-batch state for bit-exact replay: every device array that carries env state
  * between launches (agent records, seeds, tile plans, all RNG streams with their buffered halves,
- * visited bitsets, both car banks, traffic records, spawner lists, map queue, counters) as one host
+ * visited bitsets, the car slots, traffic records with the persisted lane-square occupancy counters,
+ * spawner lists, map queue, counters) as one host
  * blob.  pgtg_state_size gives the blob size; pgtg_load_state accepts only a blob dumped from a handle
  * of the same config (checked by a hash of every configuration field) and batch size.  Outputs are not state: call pgtg_observe after a load to
  * re-emit the observations.  Both synchronise.  (No reference equivalent: PGTGEnv deep-copies
