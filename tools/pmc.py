@@ -41,7 +41,7 @@ def main():
     rec = {"workload": wl, "envs": envs, "tag": tag, "unit": "bytes per step launch",
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate bench.py runs; "
                      "read bytes = 2 x FETCH_SIZE (gfx950 16-B/lane streaming-read calibration), "
-                     "write bytes = WRITE_SIZE; median over the step dispatches after the first 10"}
+                     "write bytes = WRITE_SIZE; median over the step dispatches after the first 10 (tools/gpu_profile.sh: 200 warm-up + 60 steps)"}
     total = 0.0
     for k in ("k_env", "k_traffic"):
         if k not in fetch or k not in write:
