@@ -146,8 +146,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--timing-every", type=int, default=0,
-                    help="bracket every n-th step launch with HIP events (kernel duration for the roofline); "
-                         "default max(1, steps // 16): at least 16 timed launches")
+                    help="launches of the event-bracketed kernel pass after the timed window (kernel duration "
+                         "for the roofline); default max(16, min(64, steps))")
     ap.add_argument("--dist", action="store_true",
                     help="initialise the process group and run the counter all-reduce on the device even "
                          "at world size 1 (RCCL check on a one-GPU box; use under torch.distributed.run)")
@@ -181,7 +181,7 @@ def main():
     from pgtg_amd.build import build
     build()  # no-op when the in-tree library is current (file-locked across ranks)
     from pgtg_amd.config import make_spec
-    from pgtg_amd.dist import Shard, reduce_counters
+    from pgtg_amd.dist import Shard, reduce_counters, reduce_sum
     from pgtg_amd.vector import PGTGVecEnv
 
     cfg_idx, desc, n_total, kwargs = WORKLOADS[args.workload]
@@ -205,28 +205,44 @@ def main():
         env.step_actions(actions[t])
     torch.cuda.synchronize(dev)
     steps0, eps0 = env.counters()
-    timing_every = args.timing_every or max(1, args.steps // 16)
-    env.enable_timing(timing_every)
-    env.timing_read(reset=True)
+    maps0 = env.queue_maps()
+    env.enable_timing(0)  # no per-launch events inside the timed window
+    # one event pair around the whole window on the stream the kernels run on (torch's current
+    # stream, which the env binds): the device time of the K launches, launch gaps included
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record()
     if args.per_step:
         for t in range(args.warmup, args.warmup + args.steps):
             env.step_actions(actions[t])
     else:  # one host call queues the K launches (pgtg_step_many), same kernels and results
         env.step_many(actions[args.warmup:args.warmup + args.steps])
+    ev1.record()
     torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    window_ms = ev0.elapsed_time(ev1)
+    steps1, eps1 = env.counters()
+    maps1 = env.queue_maps()
+    # the step kernel's own launch duration for the roofline, after the timed window: every launch of
+    # a second pass bracketed with a HIP event pair (the same kernels on the same stream, continuing
+    # the rollout; not part of `value`)
+    kpass = args.timing_every or max(16, min(64, args.steps))
+    env.enable_timing(1)
+    env.timing_read(reset=True)
+    for k in range(kpass):  # (every rank: the ranks' trajectories stay those of a one-GPU run)
+        env.step_random(act_seed ^ 0xA5A5, k, env_offset=shard.offset)
+    torch.cuda.synchronize(dev)
     kern_ms, launches = env.timing_read(reset=True)
     env.enable_timing(0)
-    steps1, eps1 = env.counters()
     # RCCL (nccl backend) all-reduce: global env-step / episode counters (sum), slowest rank's time (max)
     total_steps, total_eps, t_max = reduce_counters(steps1 - steps0, eps1 - eps0, elapsed, device=red_dev,
                                                     force=args.dist)
+    (total_maps,) = reduce_sum([maps1 - maps0], device=red_dev, force=args.dist)
     collective = {"backend": dist.get_backend() if use_dist else None, "executed": use_dist,
                   "device_tensors": bool(use_dist and red_dev is not None), "world": world}
     value = total_steps / t_max
@@ -263,6 +279,9 @@ def main():
                        "map": f"{spec.width}x{spec.height}", "traffic_density": spec.traffic_density,
                        "autoreset": True, "parallelism": f"dp{world} (env shards, no data-path collective)"},
             "episodes": total_eps, "collective": collective,
+            # k_envq: maps its helper waves generated in the window for later episodes (the rings start
+            # full: reset fills them, k_qfill), beside the episodes that took a queued map
+            "queue_maps_generated": total_maps if maps1 else None,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                          "frac": achieved / peak if peak > 0 else None, "traffic": traffic,
                          "traffic_source": traffic_src,
@@ -272,6 +291,8 @@ def main():
                          "peak_spec": PEAK_HBM_SPEC_GBS, "frac_spec": achieved / PEAK_HBM_SPEC_GBS,
                          "kernel": env.step_kernel() + " (step + in-kernel auto-reset)",
                          "avg_kernel_us": avg_kernel_s * 1e6, "timed_launches": launches,
+                         "kernel_timing": "HIP event pair per launch, separate pass after the timed window",
+                         "window_gpu_us_per_step": 1e3 * window_ms / args.steps,
                          "alg_bytes_per_launch": alg, "alg_model": "SURVEY.md 8(d)",
                          "resets_per_launch": resets_per_launch, "cars_per_env": cars,
                          "envs_per_workgroup": env.launch_info()[0], "lds_bytes": env.launch_info()[1],

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PGTG_ABI_VERSION 5
+#define PGTG_ABI_VERSION 6
 
 /* status codes (Python facade maps them to the reference's exception types) */
 #define PGTG_OK 0
@@ -42,7 +42,7 @@ extern "C" {
 
 /* limits of this build */
 #define PGTG_MAX_TILES 256     /* width*height of the tile map (16 x 16; traffic: squares <= 255 per side) */
-#define PGTG_MAX_CHANNELS 48   /* observation keys (the reference's feature vocabulary has 51 distinct names) */
+#define PGTG_MAX_CHANNELS 128  /* observation keys: distinct feature names (the vocabulary has 51; unknown names give zero channels) */
 #define PGTG_MAX_RULES 8       /* traffic rules: the triggered-rule mask output is one byte per env */
 #define PGTG_MAX_WINDOW 31     /* observation window side (9 fixed, 2*s+1 sliding, s <= 15) */
 
@@ -142,7 +142,8 @@ typedef struct {
   int32_t terminated, flat_tire, phase, elapsed;
   int32_t n_cars, next_car_id, path_len, error;
   uint32_t spawn_counter;
-  uint64_t seed, used_subgoals;       /* bit t: tile t's subgoal used (tiles 0..63) */
+  uint64_t seed;
+  uint64_t used_subgoals[4];           /* bit t%64 of word t/64: tile t's subgoal used (all 256 tiles) */
   int32_t n_spawners, car_tail;        /* car slots in use (cars + empty slots before the last car) */
 } PgtgEnvState;
 
@@ -219,6 +220,10 @@ int pgtg_observe(pgtg_handle* h);
 int pgtg_car_digest(pgtg_handle* h, uint64_t* out_dev);
 /* steps (env-steps executed) and episodes (resets) since create, summed over envs; synchronises. */
 int pgtg_get_counters(pgtg_handle* h, uint64_t* env_steps, uint64_t* episodes);
+/* Map-queue ring entries generated since create (k_qfill after resets + the step launches' helper
+ * waves; 0 for handles without the queue): a window's delta beside its episode delta shows that the
+ * maps the episodes consumed were generated in the window.  Synchronises. */
+int pgtg_get_queue_maps(pgtg_handle* h, uint64_t* maps);
 /* Number of envs whose last step reported an error (PGTG_E_DONE / PGTG_E_MAP); synchronises. */
 int pgtg_error_count(pgtg_handle* h, uint64_t* n_errors, int32_t* first_code);
 /* Measured HBM denominator of the roofline: a 16-B/lane stream copy of `bytes` between two device

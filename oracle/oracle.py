@@ -14,7 +14,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 
-MAX_FEATURES = 48
+MAX_FEATURES = 128
 MAX_RULES = 8
 
 

@@ -14,9 +14,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 # PGTG_LIB selects another build of the same library (test variants, pgtg_amd/build.py VARIANTS)
 LIB_PATH = os.environ.get("PGTG_LIB") or os.path.join(PKG, "libpgtg_hip.so")
 
-PGTG_ABI_VERSION = 5
+PGTG_ABI_VERSION = 6
 MAX_TILES = 256
-MAX_CHANNELS = 48
+MAX_CHANNELS = 128
 MAX_RULES = 8
 
 PGTG_OK = 0
@@ -32,7 +32,7 @@ EXPORTED = [
     "pgtg_get_map_plan", "pgtg_get_squares", "pgtg_set_rules", "pgtg_set_agent", "pgtg_add_car", "pgtg_observe", "pgtg_get_counters",
     "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_launch_info", "pgtg_occupancy", "pgtg_step_kernel", "pgtg_last_error", "pgtg_enable_timing",
     "pgtg_timing_read", "pgtg_measure_hbm", "pgtg_state_size", "pgtg_dump_state", "pgtg_load_state",
-    "pgtg_set_to_state", "pgtg_car_digest",
+    "pgtg_set_to_state", "pgtg_car_digest", "pgtg_get_queue_maps",
 ]
 
 
@@ -79,7 +79,7 @@ class PgtgOutputs(C.Structure):
 class PgtgEnvState(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("x", "y", "vx", "vy", "terminated", "flat_tire", "phase", "elapsed",
                                          "n_cars", "next_car_id", "path_len", "error")] + [
-        ("spawn_counter", C.c_uint32), ("seed", C.c_uint64), ("used_subgoals", C.c_uint64),
+        ("spawn_counter", C.c_uint32), ("seed", C.c_uint64), ("used_subgoals", C.c_uint64 * 4),
         ("n_spawners", C.c_int32), ("car_tail", C.c_int32)]
 
 
@@ -129,6 +129,7 @@ def lib():
         "pgtg_observe": ([vp], C.c_int),
         "pgtg_get_counters": ([vp, C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "pgtg_car_digest": ([vp, vp], C.c_int),
+        "pgtg_get_queue_maps": ([vp, C.POINTER(u64)], C.c_int),
         "pgtg_error_count": ([vp, C.POINTER(u64), C.POINTER(i32)], C.c_int),
         "pgtg_window": ([vp], C.c_int),
         "pgtg_num_envs": ([vp], u64),

@@ -81,7 +81,7 @@ DEFAULT_RULES = [
     },
 ]
 MAX_RULES = 8
-MAX_CHANNELS = 48
+MAX_CHANNELS = 128
 
 
 def feature_channels(features: list[str]) -> list[tuple[str, int]]:

@@ -2948,6 +2948,11 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       }
       if (l < kQueueDepth) refill(k, l);
     }
+    if (lane == 0) {  // maps generated (S.counters[2]): the heads, then one per lane for levels 1..
+      int rest = 0;
+      for (int l = 1; l < kQueueDepth; l++) rest += F[l];
+      atomicAdd(&S.counters[2], (unsigned long long)(F[0] + min(rest, kQueueLanes)));
+    }
     STAMP(7);
     return;
   }
@@ -3074,6 +3079,38 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   if (tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
   stagger_record(L, S, t_start);
   STAMP(6);
+}
+
+// Fill every env's map ring (after a reset, whose k_env launch generated the current episodes' maps and
+// emptied the rings): one lane per env generates the missing entries in ring order, spawn counters
+// spawn, spawn + 5, spawn + 10 -- the maps k_envq's helper wave would generate over the first launches
+// (while the env waves wait for the heads), so that the first step launches run in the steady state the
+// rings keep from then on.  The entries are a function of (seed, spawn counter) alone: results are
+// unchanged.
+template <bool BIG>
+__global__ void __launch_bounds__(kBlock) k_qfill(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
+                                                  DevState S, int pdw) {
+  extern __shared__ uint32_t lds[];
+  const DevCfg& c = *cfg;
+  stage_tables(gtab, false);
+  lds_barrier();
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  uint32_t made = 0;
+  if (i < S.n) {
+    const uint32_t qs = S.qstate[i], qn = qs & 3u, qh = (qs >> 2) & 3u;
+    if (qn < (uint32_t)kQueueDepth) {
+      const uint32_t spawn = S.rec[i].b.y;  // EnvRec w5
+      uint16_t* plan = reinterpret_cast<uint16_t*>(lds + threadIdx.x * pdw);
+      for (uint32_t l = qn; l < (uint32_t)kQueueDepth; l++)
+        gen_queue_entry<BIG>(c, S, i, spawn + 5u * l, plan, pdw,
+                             S.qbuf + (i * kQueueDepth + (qh + l) % (uint32_t)kQueueDepth) * (uint64_t)c.qrec_dw);
+      S.qstate[i] = (uint8_t)(kQueueDepth | qh << 2);
+      made = (uint32_t)kQueueDepth - qn;
+    }
+  }
+  // maps generated (S.counters[2]): one atomic per wave
+  const uint32_t wsum = (uint32_t)__popcll(__ballot(made & 1u)) + 2u * (uint32_t)__popcll(__ballot(made & 2u));
+  if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(&S.counters[2], (unsigned long long)wsum);
 }
 
 #ifdef PGTG_STAMPS
@@ -3826,7 +3863,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
   ALLOC(S.seed, n);
   ALLOC(S.plan, n * (uint64_t)c.plan_stride);
   ALLOC(S.err, n);
-  ALLOC(S.counters, 2);
+  ALLOC(S.counters, 4);  // env steps, episodes, map-queue entries generated (state blob: the first two)
   ALLOC(S.wg_ticks, 1);
   DevStream* streams[4] = {&S.car, &S.ice, &S.broken, &S.sand};
   int needs[4] = {c.need_car, c.need_ice, c.need_broken, c.need_sand};
@@ -4015,6 +4052,24 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
   return PGTG_OK;
 }
 
+// After a reset launch of a map-queue handle: fill the rings the reset emptied (k_qfill).
+static int queue_fill(pgtg_handle* h) {
+  if (!h->L.queue || !h->S.qbuf) return PGTG_OK;
+#ifdef PGTG_TUNING
+  if (const char* e = getenv("PGTG_QFILL"))
+    if (!atoi(e)) return PGTG_OK;
+#endif
+  const int pdw = h->L.plan_stride_dw;
+  const size_t lds = (size_t)4 * kBlock * pdw;
+  const void* fn = h->hcfg.nt > kSmallTiles ? (const void*)k_qfill<true> : (const void*)k_qfill<false>;
+  if (lds > 64 * 1024) HIPCHK(h, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const uint64_t blocks = (h->n + kBlock - 1) / kBlock;
+  void* args[] = {&h->dcfg, &h->dtab, &h->S, (void*)&pdw};
+  HIPCHK(h, hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(kBlock), args, lds, h->stream));
+  HIPCHK(h, hipGetLastError());
+  return PGTG_OK;
+}
+
 int pgtg_reset(pgtg_handle* h, const uint64_t* seeds_host, uint64_t seed_base, const uint8_t* mask_dev) {
   if (!h) return PGTG_E_INVALID;
   HIPCHK(h, hipSetDevice(h->device));
@@ -4025,12 +4080,14 @@ int pgtg_reset(pgtg_handle* h, const uint64_t* seeds_host, uint64_t seed_base, c
                        seed_base, (uint64_t)0);
     HIPCHK(h, hipGetLastError());
   }
-  return launch(h, nullptr, mask_dev, MODE_RESET_SEEDED);
+  if (int rc = launch(h, nullptr, mask_dev, MODE_RESET_SEEDED)) return rc;
+  return queue_fill(h);
 }
 
 int pgtg_reset_unseeded(pgtg_handle* h, const uint8_t* mask_dev) {
   if (!h) return PGTG_E_INVALID;
-  return launch(h, nullptr, mask_dev, MODE_RESET_UNSEEDED);
+  if (int rc = launch(h, nullptr, mask_dev, MODE_RESET_UNSEEDED)) return rc;
+  return queue_fill(h);
 }
 
 int pgtg_step(pgtg_handle* h, const uint8_t* actions_dev) {
@@ -4086,12 +4143,12 @@ int pgtg_get_env_state(pgtg_handle* h, uint64_t env, PgtgEnvState* st) {
   st->path_len = (int)(r.a.z >> 20);
   st->elapsed = (int)r.a.w;
   st->spawn_counter = r.b.y;
-  st->used_subgoals = (uint64_t)r.b.z | ((uint64_t)r.b.w << 32);
-  if (h->hcfg.nt > kSmallTiles) {  // maps of > 64 tiles mark the plan words: report tiles 0..63
+  st->used_subgoals[0] = (uint64_t)r.b.z | ((uint64_t)r.b.w << 32);
+  if (h->hcfg.nt > kSmallTiles) {  // maps of > 64 tiles mark the plan words (kPlanUsed)
     std::vector<uint16_t> p(h->hcfg.plan_stride);
     HIPCHK(h, hipMemcpy(p.data(), h->S.plan + env * (uint64_t)h->hcfg.plan_stride, p.size() * 2, hipMemcpyDeviceToHost));
-    st->used_subgoals = 0;
-    for (int t = 0; t < 64; t++) st->used_subgoals |= (uint64_t)((p[t] & kPlanUsed) != 0) << t;
+    st->used_subgoals[0] = 0;
+    for (int t = 0; t < h->hcfg.nt; t++) st->used_subgoals[t >> 6] |= (uint64_t)((p[t] & kPlanUsed) != 0) << (t & 63);
   }
   st->seed = seed;
   st->error = -(int)e;
@@ -4481,6 +4538,16 @@ int pgtg_get_counters(pgtg_handle* h, uint64_t* env_steps, uint64_t* episodes) {
   HIPCHK(h, hipMemcpy(c, h->S.counters, sizeof c, hipMemcpyDeviceToHost));
   if (env_steps) *env_steps = c[0];
   if (episodes) *episodes = c[1];
+  return PGTG_OK;
+}
+
+int pgtg_get_queue_maps(pgtg_handle* h, uint64_t* maps) {
+  if (!h || !maps) return PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  unsigned long long c[3];
+  HIPCHK(h, hipMemcpy(c, h->S.counters, sizeof c, hipMemcpyDeviceToHost));
+  *maps = c[2];
   return PGTG_OK;
 }
 

@@ -48,3 +48,14 @@ def reduce_counters(env_steps: int, episodes: int, elapsed_s: float, device=None
     dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
     dist.all_reduce(tim, op=dist.ReduceOp.MAX)
     return int(cnt[0].item()), int(cnt[1].item()), float(tim[0].item())
+
+
+def reduce_sum(values, device=None, force: bool = False) -> list[int]:
+    """Element-wise sum of integer counters over ranks (identity without a process group)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or (dist.get_world_size() == 1 and not force):
+        return [int(v) for v in values]
+    t = torch.tensor([int(v) for v in values], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(x) for x in t.tolist()]

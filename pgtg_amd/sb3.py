@@ -4,19 +4,53 @@ pgtg/train.py:54-55).
 `PGTGSB3VecEnv(num_envs, max_episode_steps=100, **PGTGEnv kwargs)` follows SB3's `VecEnv` protocol
 (duck-typed, stable_baselines3 need not be installed): `reset() -> obs`, `step_async(actions)` /
 `step_wait() -> (obs, rewards, dones, infos)` with `infos[i]["terminal_observation"]` and
-`infos[i]["TimeLimit.truncated"]` for finished envs.  Observations are the `FlattenObservation`
+`infos[i]["TimeLimit.truncated"]` for finished envs (`infos` a lazy sequence, `VecInfos`: no per-env
+Python loop in the step).  Observations are the `FlattenObservation`
 vectors of pgtg/train.py:40 (pgtg_amd/flat.py), as float32 numpy arrays because SB3 policies take
 host arrays; `max_episode_steps` is the `TimeLimit(100)` wrapper of pgtg/train.py:39, applied
 in-kernel (truncation and auto-reset in the same step).
 """
 from __future__ import annotations
 
+from collections.abc import Sequence
 from typing import Any
 
 import numpy as np
 
 from .flat import flat_dim, flatten_obs
 from .vector import PGTGVecEnv
+
+
+class VecInfos(Sequence):
+    """SB3's per-env `infos` list without per-env Python work in the step: the batch's arrays are kept
+    and env i's dict ({"terminal_observation", "TimeLimit.truncated"} when it finished, "cost" with
+    separate_reward_cost) is built when it is read, so a step costs O(1) host work whatever the batch
+    size; callers that read every entry pay for what they read."""
+
+    def __init__(self, dones, truncated, final, cost):
+        self._dones, self._trunc, self._final, self._cost = dones, truncated, final, cost
+
+    def __len__(self) -> int:
+        return len(self._dones)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        d: dict[str, Any] = {}
+        if self._dones[i]:
+            d["terminal_observation"] = self._final[i]
+            d["TimeLimit.truncated"] = bool(self._trunc[i])
+        if self._cost is not None:
+            d["cost"] = float(self._cost[i])
+        return d
+
+    def finished(self) -> np.ndarray:
+        """Indices of the envs whose episode ended this step (vectorised access)."""
+        return np.nonzero(self._dones)[0]
 
 
 class PGTGSB3VecEnv:
@@ -59,17 +93,9 @@ class PGTGSB3VecEnv:
         rew = reward.to(torch.float32).cpu().numpy()
         term_h, trunc_h = term.cpu().numpy().astype(bool), trunc.cpu().numpy().astype(bool)
         dones = term_h | trunc_h
-        out_infos: list[dict[str, Any]] = [{} for _ in range(self.num_envs)]
-        if dones.any():
-            final = flatten_obs(self.spec, infos["final_observation"]).cpu().numpy()
-            for i in np.nonzero(dones)[0]:
-                out_infos[i]["terminal_observation"] = final[i]
-                out_infos[i]["TimeLimit.truncated"] = bool(trunc_h[i] and not term_h[i])
-        if "cost" in infos:
-            cost = infos["cost"].cpu().numpy()
-            for i in range(self.num_envs):
-                out_infos[i]["cost"] = float(cost[i])
-        return flat, rew, dones, out_infos
+        final = flatten_obs(self.spec, infos["final_observation"]).cpu().numpy() if dones.any() else None
+        cost = infos["cost"].cpu().numpy() if "cost" in infos else None
+        return flat, rew, dones, VecInfos(dones, trunc_h & ~term_h, final, cost)
 
     def step(self, actions):
         self.step_async(actions)

@@ -249,7 +249,9 @@ class PGTGVecEnv:
     def env_state(self, i: int) -> dict:
         st = _abi.PgtgEnvState()
         _check(self._lib.pgtg_get_env_state(self._h, i, C.byref(st)), self._h)
-        return {f: getattr(st, f) for f, _ in st._fields_}
+        d = {f: getattr(st, f) for f, _ in st._fields_}
+        d["used_subgoals"] = sum(int(w) << (64 * k) for k, w in enumerate(st.used_subgoals))  # bit t: tile t
+        return d
 
     def cars(self, i: int):
         import numpy as np
@@ -372,6 +374,12 @@ class PGTGVecEnv:
         a, b = C.c_uint64(), C.c_uint64()
         _check(self._lib.pgtg_get_counters(self._h, C.byref(a), C.byref(b)), self._h)
         return a.value, b.value
+
+    def queue_maps(self) -> int:
+        """Map-queue ring entries generated since create (0 without the queue)."""
+        m = C.c_uint64()
+        _check(self._lib.pgtg_get_queue_maps(self._h, C.byref(m)), self._h)
+        return m.value
 
     def enable_timing(self, every: int = 1):
         """Bracket every `every`-th step launch with a HIP event pair (0: off)."""

@@ -79,3 +79,14 @@ def test_json_map_loader_roundtrip(tmp_path):
     old.write_text('{"width": 1, "height": 1, "map": [[{"exits": [0, 1, 0, 1]}]]}')
     with pytest.raises(KeyError):
         C.json_file_to_map_plan(str(old))
+
+
+def test_feature_vocabulary_and_unknown_names_fit():
+    """The whole vocabulary plus unknown names (zero channels) is accepted, as the reference accepts
+    any feature list; past PGTG_MAX_CHANNELS distinct keys the build refuses."""
+    import pytest
+    names = ["walls", "goals", "traffic", "traffic_light"] + list(C._GENERIC) + [f"x{k}" for k in range(14)]
+    s = C.make_spec(random_map_width=4, random_map_height=4, features_to_include_in_observation=names)
+    assert len(s.channels) == 61
+    with pytest.raises(ValueError):
+        C.make_spec(features_to_include_in_observation=[f"x{k}" for k in range(C.MAX_CHANNELS + 1)])

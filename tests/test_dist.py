@@ -8,7 +8,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pgtg_amd.dist import Shard, reduce_counters
+from pgtg_amd.dist import Shard, reduce_counters, reduce_sum
 
 
 def _free_port():
@@ -25,7 +25,8 @@ def _worker(rank, world, port, n_local, q):
     sh = Shard(rank, world, n_local)
     steps, eps = n_local * 10, rank + 3
     tot_steps, tot_eps, t = reduce_counters(steps, eps, 1.0 + rank)
-    q.put((rank, sh.offset, sh.global_ids([0, n_local - 1]), tot_steps, tot_eps, t))
+    maps = reduce_sum([100 * (rank + 1), rank])
+    q.put((rank, sh.offset, sh.global_ids([0, n_local - 1]), tot_steps, tot_eps, t, maps))
     dist.destroy_process_group()
 
 
@@ -45,7 +46,9 @@ def test_two_rank_shards_and_counters():
     assert res[1][2] == [n_local, 2 * n_local - 1]  # contiguous global ids == seeds
     for r in res:
         assert r[3] == world * n_local * 10 and r[4] == 3 + 4 and r[5] == 2.0
+        assert r[6] == [300, 1]
 
 
 def test_single_process_identity():
     assert reduce_counters(5, 2, 0.5) == (5, 2, 0.5)
+    assert reduce_sum([7, 9]) == [7, 9]

@@ -6,9 +6,12 @@ formulas to each other), so whole batches are compared without copying them to t
 
   configs[1]  4 096 envs x 100 steps, 3x3 maps                    (SURVEY.md 8(d) cfg 2)
   configs[3]  262 144 envs x 20 steps, 3x3 maps, in-kernel resets
-  configs[4]  1 048 576 envs x 10 steps, 5x5 maps (the bench line; grid indexing past 2^20 envs)
-  configs[2]  65 536 envs x 40 steps, 5x5 maps, traffic 0.5, with every env's car list in the
-              digest (id, square, route, profile, patience, delay of every car after every step), plus
+  configs[4]  1 048 576 envs x 40 steps, 5x5 maps (the bench line; grid indexing past 2^20 envs; the
+              map-queue rings through their refill steady state: a ring holds 3 episodes, a
+              workgroup's helper wave refills <= 64 of them per launch)
+  configs[2]  65 536 envs x 200 steps, 5x5 maps, traffic 0.5, with every env's car list in the
+              digest (id, square, route, profile, patience, delay of every car after every step: the
+              persisted occupancy counters, packing ticks, patience past patience_level*10), plus
               256 envs x 120 steps of cautious driving with the car lists compared (patience,
               crowded squares, spawner lists beyond the staged first 24)
   feature variants at batch sizes of every launch shape, incl. forced workgroup/sub-batch shapes.
@@ -62,12 +65,17 @@ def _compare(spec, n, T, tune=None, tag="", min_distinct=1000):
     assert bad.size == 0, (f"{tag} {kern} {shape}: {len(bad)} (step, env) digests differ, first {bad[:8].tolist()}")
 
 
+# every feature name of the reference's vocabulary (pgtg/environment.py:1387-1445) plus names it does
+# not know (all-zero channels): 61 observation keys
+ALL_FEATURES = (["walls", "goals", "traffic", "traffic_light"] + list(cfg._GENERIC) +
+                [f"unknown feature {k}" for k in range(14)])
+
 CASES = {
     # name: (envs, steps, kwargs, launch-shape overrides)
     "cfg2_all_4096x100": (4096, 100, dict(random_map_width=3, random_map_height=3), None),
     "cfg4_all_262144x20": (262144, 20, dict(random_map_width=3, random_map_height=3), None),
-    "cfg5_all_1048576x10": (1048576, 10, dict(random_map_width=5, random_map_height=5), None),
-    "cfg3_all_65536x40": (65536, 40, dict(random_map_width=5, random_map_height=5, traffic_density=0.5), None),
+    "cfg5_all_1048576x40": (1048576, 40, dict(random_map_width=5, random_map_height=5), None),
+    "cfg3_all_65536x200": (65536, 200, dict(random_map_width=5, random_map_height=5, traffic_density=0.5), None),
     # feature variants over the launch shapes (16/32/64/128/256 envs per workgroup, sub-batched images)
     "obstacles_40000": (40000, 15, dict(random_map_width=4, random_map_height=4, random_map_obstacle_probability=1.0,
                                         random_map_ice_probability_weight=1, random_map_broken_road_probability_weight=1,
@@ -85,6 +93,9 @@ CASES = {
     "sliding_traffic_6000": (6000, 8, dict(random_map_width=5, random_map_height=5, use_sliding_observation_window=True,
                                            sliding_observation_window_size=4, use_next_subgoal_direction=True,
                                            traffic_density=0.2), None),
+    "features_all_names_3000": (3000, 10, dict(random_map_width=4, random_map_height=4, traffic_density=0.3,
+                                               random_map_obstacle_probability=0.5,
+                                               features_to_include_in_observation=ALL_FEATURES), None),
     "cfg2_wg256_sub32": (4096, 40, dict(random_map_width=3, random_map_height=3),
                          dict(envs_per_block=256, obs_sub=32)),
     "cfg5_wg256": (65536, 20, dict(random_map_width=5, random_map_height=5), dict(envs_per_block=256)),

@@ -84,6 +84,7 @@ def test_sb3_adapter_flattened_obs_and_terminal_infos():
     for t in range(20):
         acts = rng.integers(0, 9, N)
         obs, rew, dones, infos = env.step(acts)
+        assert len(infos) == N and list(infos.finished()) == list(np.nonzero(dones)[0])
         for i in range(N):
             r = orcs[i].step(int(acts[i]))
             elapsed[i] += 1
@@ -97,6 +98,8 @@ def test_sb3_adapter_flattened_obs_and_terminal_infos():
                 r = orcs[i].reset(None)
                 elapsed[i] = 0
                 seen_done += 1
+            else:
+                assert infos[i] == {}
             assert np.array_equal(obs[i], flatten_obs(spec, _oracle_obs_dict(spec, r)).numpy()[0]), (t, i)
     assert seen_done > 0
     env.close()

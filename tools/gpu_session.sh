@@ -5,6 +5,8 @@
 #   tests:<expr>     pytest -m gpu -k <expr>
 #   smoke            __graft_entry__.smoke()
 #   bench            the default bench line (configs[4], with the CPU baseline)
+#   driver           the driver's own line: bench.py --gpus 1 --steps 20 --warmup 5
+#   ramp:<wl>        per-launch kernel time of the first 80 launches after a reset (tools/ramp.py)
 #   bench:<wl>       bench.py --workload <wl> --steps 200 --warmup 20
 #   benchlong:<wl>   bench.py --workload <wl> with the default 1000-step window
 #   rccl             bench.py under torch.distributed.run, one rank, nccl backend, --dist (RCCL init +
@@ -39,6 +41,12 @@ for S in "$@"; do
     bench)
       timeout -k 10 400 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
       cat $O/bench_default.json ;;
+    driver)
+      timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err || { tail -20 $O/bench_driver.err; exit 1; }
+      python tools/bench_line.py $O/bench_driver.json ;;
+    ramp:*)
+      timeout -k 10 300 python -u tools/ramp.py ${S#ramp:} > $O/ramp_${S#ramp:}.log 2>&1 || { tail -20 $O/ramp_${S#ramp:}.log; exit 1; }
+      tail -6 $O/ramp_${S#ramp:}.log ;;
     benchlong:*)
       W=${S#benchlong:}
       timeout -k 10 400 python -u bench.py --workload $W --no-cpu-baseline > $O/benchlong_$W.json 2> $O/benchlong_$W.err || { tail -20 $O/benchlong_$W.err; exit 1; }
