@@ -167,17 +167,25 @@ struct DevState {
   // coalesced access.  w0 = x | y<<8 | route<<16 | profile<<21 | delay<<24 (bit 31: empty slot, a
   // despawned car), w1 = patience counter, id = car id.  Survivors are rewritten in place, respawns
   // appended behind the tail, the slots compacted when a tick's respawns could overrun them.
-  // traf[n] = {n_cars | n_spawners<<16, next_id, tail (slots in use), occ_valid}
+  // traf[n] = {n_cars | n_spawners<<16, next_id, tail (slots in use), flags}: flags bit 0 = the
+  // occupancy counters are exact for the env's current cars (else k_env rebuilds them from the car
+  // slots), bit 1 = fresh: the env's cars and counters are still in its staging block (below).
   // occ: the 4-bit lane-square occupancy counters (nt * 4 words per env, slot-major [word][n]) as the
-  // last launch left them; traf.w == 1 when they are exact for the env's current cars (written by
-  // k_traffic for fresh traffic, by k_env after a step whose counters never saturated), else k_env
-  // rebuilds them from the car slots
+  // last launch left them.
+  // fresh: per env one contiguous staging block ([n][fresh_dw]) that k_traffic writes for an env it
+  // gave initial traffic -- w0 of its cars at [0, k) (patience 0 and id = slot index implied), the
+  // counters at [fresh_occ, fresh_occ + nt*4) -- as runs of consecutive words instead of one 4-byte
+  // store per slot row of scattered envs; the env's next car pass reads its cars from there and
+  // writes them (with their ids) to the slot rows beside every other env's.
   uint32_t* car_w0;
   uint32_t* car_w1;
   uint32_t* car_id;
   uint4* traf;
   uint32_t* occ;          // [nt * 4][n] or null
-  uint16_t* spawners;     // [max_spawners][n] square codes x | y<<8, x-major order
+  uint32_t* fresh;        // [n][fresh_dw] or null
+  uint16_t* spawners;     // [n][sp_pitch] square codes x | y<<8, x-major order (env-major: written once
+                          // per episode by k_traffic as contiguous runs, read 24 at a time by k_env)
+  uint32_t sp_pitch, fresh_dw, fresh_occ;
   uint32_t* tr_list;      // [n] envs k_env reset this launch (k_traffic's work list)
   uint32_t* tr_count;     // [2] list lengths, alternating launches
   // map queue (k_envq): per env a ring of kQueueDepth pre-generated episode maps, entry = plan

@@ -363,6 +363,11 @@ struct CarSlots {
   }
   __device__ __forceinline__ uint64_t at(int k) const { return (uint64_t)k * n; }
 };
+// An env's staging block (DevState::fresh): w0 of its fresh cars at [0, k), counters at fresh_occ.
+__device__ __forceinline__ gu32* fresh_block(const DevState& S, uint64_t i) {
+  return (gu32*)(S.fresh + i * (uint64_t)S.fresh_dw);
+}
+constexpr uint32_t kTrafOccValid = 1u, kTrafFresh = 2u;  // traf.w flags
 
 // ------------------------------------------------------------------------------------------------
 // reset: seeding, procedural map, compilation, start square  (pgtg/environment.py:581-656)
@@ -862,6 +867,7 @@ __device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, int
 
 struct TrafState {
   uint32_t n_cars, n_spawners, next_id, tail;  // tail: car slots in use (cars and empty slots)
+  uint32_t fresh;  // the cars are still in the env's staging block (traf.w kTrafFresh)
 };
 
 // spawner squares of local column lx of tile (tx, ty): lane-data spawners (dead ends) plus the
@@ -925,21 +931,20 @@ __device__ __forceinline__ void car_squares(const DevCfg& c, const Plan& pl, con
     q[u].nr = __popc(q[u].rl);
   }
 }
-__device__ __forceinline__ void store_new_car(const CarSlots& cs, uint64_t a, const CarSquare& q, int route, int prof, int m) {
-  cs.w0[a] = (uint32_t)q.x | (uint32_t)q.y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
-  cs.w1[a] = 0u;
-  cs.id[a] = (uint32_t)m;
+// A fresh car m of the env: w0 into the env's staging block (patience 0 and id m are implied by the
+// fresh flag).  The lanes of a group write runs of consecutive words.
+__device__ __forceinline__ void store_new_car(gu32* fw, const CarSquare& q, int route, int prof, int m) {
+  fw[m] = (uint32_t)q.x | (uint32_t)q.y << 8 | (uint32_t)route << 16 | (uint32_t)prof << 21;
 }
 
 // The per-car draws on one lane, in id order: random() -> profile, then choice(routes) when the
 // square has more than one route (numpy draws nothing for one).  `cr` enters as the stream after the
 // shuffle and leaves after the last car.
-__device__ __forceinline__ int cars_serial(const DevCfg& c, const CarSlots& cs, const Plan& pl, const uint16_t* out, int k,
-                                        int at, uint32_t* CR, Pcg& cr) {
+__device__ __forceinline__ int cars_serial(const DevCfg& c, const CarSlots& cs, gu32* fw, const Plan& pl, const uint16_t* out,
+                                        int k, int at, uint32_t* CR, Pcg& cr) {
   const ProfileCdf pcdf = pin_profile_cdf(c);
   PcgAhead ca = ahead_init(cr);
   CR[0] = CR[1] = CR[2] = 0u;
-  uint64_t a_m = cs.at(0);
   for (int m = 0; m < k; m++) {
     const CarSquare q = car_square(c, pl, out[m]);
     if (q.tile == at) CR[q.sq >> 5] |= 1u << (q.sq & 31);
@@ -947,8 +952,7 @@ __device__ __forceinline__ int cars_serial(const DevCfg& c, const CarSlots& cs, 
     const uint64_t u = ahead_draw(ca, false, 0u);
     const int prof = profile_of(pcdf, u);
     const uint32_t rk = q.nr > 1u ? (uint32_t)ahead_draw(ca, true, q.nr) : 0u;
-    store_new_car(cs, a_m, q, sTX.lane_route[kth_bit(q.rl, (int)rk)], prof, m);
-    a_m += cs.n;
+    store_new_car(fw, q, sTX.lane_route[kth_bit(q.rl, (int)rk)], prof, m);
   }
   cr = ca.g;
   return 0;
@@ -964,7 +968,7 @@ __device__ __forceinline__ int cars_serial(const DevCfg& c, const CarSlots& cs, 
 // shift every later position: a group that meets one redoes the cars on one lane (cars_serial).
 // Returns lane 0's result; on return every lane holds the stream after the last car in `cr` and
 // lane 0 the group's agent-tile car squares in CR.
-__device__ __forceinline__ int cars_group(const DevCfg& c, const CarSlots& cs, const Plan& pl, const uint16_t* out,
+__device__ __forceinline__ int cars_group(const DevCfg& c, const CarSlots& cs, gu32* fw, const Plan& pl, const uint16_t* out,
                                           int k, int at, uint32_t* CR, Pcg& cr, int sub, int g) {
   const int q0 = (int)(threadIdx.x & 63u) - sub;  // the group's first lane
   // lane 0's post-shuffle stream to the group
@@ -1025,7 +1029,6 @@ __device__ __forceinline__ int cars_group(const DevCfg& c, const CarSlots& cs, c
     const ProfileCdf pcdf = pin_profile_cdf(c);
     PcgAhead ca = ahead_init(ls);
     int rej = 0;
-    uint64_t a_m = cs.at(m0);
     for (int m = m0; m < m1; m += kCarChunk) {
       CarSquare q[kCarChunk];
       car_squares<kCarChunk>(c, pl, out, m, m1, q);
@@ -1051,10 +1054,8 @@ __device__ __forceinline__ int cars_group(const DevCfg& c, const CarSlots& cs, c
 #pragma unroll
       for (int u = 0; u < kCarChunk; u++) route[u] = sTX.lane_route[lr[u]];
 #pragma unroll
-      for (int u = 0; u < kCarChunk; u++) {
-        if (m + u < m1) store_new_car(cs, a_m, q[u], route[u], prof[u], m + u);
-        a_m += cs.n;
-      }
+      for (int u = 0; u < kCarChunk; u++)
+        if (m + u < m1) store_new_car(fw, q[u], route[u], prof[u], m + u);
     }
     ls = ca.g;
     // the group's rejections; the stream after the last car is lane g-1's; CR merged on lane 0
@@ -1082,7 +1083,7 @@ __device__ __forceinline__ int cars_group(const DevCfg& c, const CarSlots& cs, c
     }
   }
   // one lane: the tune_kt_serial path, or a group whose draw positions a rejection shifted (redo)
-  return sub == 0 ? cars_serial(c, cs, pl, out, k, at, CR, cr) : 0;
+  return sub == 0 ? cars_serial(c, cs, fw, pl, out, k, at, CR, cr) : 0;
 }
 
 // The draws of Generator.choice(np, k, replace=False) (numpy _generator.pyx: Floyd's loop over
@@ -1161,7 +1162,6 @@ __device__ __forceinline__ void choice_draws_group(const DevCfg& c, uint16_t* ou
 __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S, uint64_t i, const Plan& pl,
                                              Pcg& cr, uint8_t* rs, TrafState& ts, int at, uint32_t* CR, int sub,
                                              int g) {
-  const uint64_t N = S.n;
   STAMP(19);
   // x-major sweep, the group's lanes on g column ranges: count, exchange the counts, then car
   // spawners -> HBM list and spawnable squares (any car lane) -> per-column prefix counts
@@ -1199,7 +1199,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
       while (m) {
         int ly = __ffs((int)m) - 1;
         m &= m - 1u;
-        if (nsp < c.max_spawners) S.spawners[(uint64_t)nsp * N + i] = (uint16_t)(x | (ty * kTile + ly) << 8);
+        if (nsp < c.max_spawners) S.spawners[i * (uint64_t)S.sp_pitch + nsp] = (uint16_t)(x | (ty * kTile + ly) << 8);
         nsp++;
       }
     }
@@ -1337,7 +1337,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
     wave_lds_sync();
     STAMP(26);  // (slot shared with k_env's removal-loop record: k_traffic runs later)
     // the cars in id order: profile and route draws -> slots 0 .. k-1 (lane-parallel, see cars_group)
-    const int e = cars_group(c, cs, pl, out, k, at, CR, cr, sub, g);
+    const int e = cars_group(c, cs, fresh_block(S, i), pl, out, k, at, CR, cr, sub, g);
     if (e) return sub == 0 ? e : 0;
     if (sub != 0) return 0;
   }
@@ -1352,7 +1352,7 @@ __device__ __forceinline__ int traffic_reset(const DevCfg& c, const DevState& S,
 // The occupancy counters of a fresh env's k cars (square codes x | y << 8 in out[0, k), one car per
 // square: no counter overflows) for k_env, which loads them instead of rebuilding them from the car
 // slots.  The g lanes of the env's group count into `cnt` (the reset scratch from rs_jj_off, free
-// once the cars exist) with LDS adds and store the nt * 4 words to S.occ.
+// once the cars exist) with LDS adds and store the nt * 4 words to the env's staging block.
 __device__ __forceinline__ void store_initial_counters(const DevCfg& c, const DevState& S, uint64_t i, const Plan& pl,
                                                        uint8_t* rs, int k, int sub, int g) {
   uint32_t* cnt = reinterpret_cast<uint32_t*>(rs + c.rs_jj_off);
@@ -1366,7 +1366,8 @@ __device__ __forceinline__ void store_initial_counters(const DevCfg& c, const De
     if (s >= 0) __hip_atomic_fetch_add(cnt + (s >> 3), 1u << ((s & 7) << 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   }
   wave_lds_sync();
-  for (int w = sub; w < nw; w += g) S.occ[(uint64_t)w * S.n + i] = cnt[w];
+  gu32* fo = fresh_block(S, i) + S.fresh_occ;
+  for (int w = sub; w < nw; w += g) fo[w] = cnt[w];
 }
 
 // The full per-env reset.  `key` = spawn counter (5 children per episode).  Returns 0 or -code.
@@ -1719,12 +1720,13 @@ __device__ __forceinline__ T sel4(int k, T a0, T a1, T a2, T a3) {
 // Exact number of cars on lane slot s while the car in slot r leaves it: slots [0, w) hold the cars
 // already moved this tick (w = r, or the packed count when the tick packs), (r, tail0) those still
 // to move, [tail0, t_out) this tick's respawns.  Rare: only once a 4-bit occupancy counter saturated.
-__device__ __noinline__ int recount_slot(const DevCfg& c, const Plan& pl, const CarSlots& cs, int r, int w, int t_out,
-                                         int s) {
+// A fresh env (fw0: its staging block) still holds the cars not yet moved, (r, tail0), there.
+__device__ __noinline__ int recount_slot(const DevCfg& c, const Plan& pl, const CarSlots& cs, const gu32* fw0, int tail0,
+                                         int r, int w, int t_out, int s) {
   int n = 0;
   for (int k = 0; k < t_out; k++) {
     if (k >= w && k <= r) continue;
-    const uint32_t w0 = cs.w0[cs.at(k)];
+    const uint32_t w0 = (fw0 && k > r && k < tail0) ? fw0[k] : cs.w0[cs.at(k)];
     if (w0 & kCarEmpty) continue;
     n += lane_slot(c, pl, (int)(w0 & 255u), (int)((w0 >> 8) & 255u)) == s ? 1 : 0;
   }
@@ -1753,6 +1755,12 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
   const int tw = c.tw, th = c.th;
   const uint32_t nsp = ts.n_spawners;
   const int tail0 = (int)ts.tail;
+  // a fresh env (initial traffic from k_traffic) reads its cars from its staging block, patience 0;
+  // every env writes the slot rows
+  const bool fresh = ts.fresh != 0;
+  gu32* const fb = fresh_block(S, i);
+  const gu32* const rb = fresh ? fb : cs.w0;
+  const uint64_t rstep = fresh ? 1ull : S.n;
   // (wave-uniform: packing is right for any list, and a uniform flag keeps the loop free of
   // exec-mask juggling around the packing writes)
   const bool pack = __any(tail0 > (int)ts.n_cars + kCompactSlack);
@@ -1762,17 +1770,26 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
   const uint64_t nst = S.n;
   // software pipeline: the next slot's words are requested before the current car is processed, so
   // their HBM latency overlaps this car's work (slot indices advance by the env stride)
-  uint64_t ar = cs.at(0), an = cs.at(tail0), ap = cs.at(0);
-  uint32_t na = cs.w0[ar], npat = cs.w1[ar], nid = 0u;
+  uint64_t ar = cs.at(0), an = cs.at(tail0), ap = cs.at(0), rr = 0;
+  uint32_t rn = 0;  // the prefetched slot (a fresh env's car ids are its slot indices)
+  uint32_t na = rb[rr], npat = cs.w1[ar], nid = 0u;
+  npat = fresh ? 0u : npat;
   if (pack) nid = cs.id[ar];
+  nid = fresh ? rn : nid;
   for (int r = 0; r < tail0; r++) {
     const uint64_t aw = ar;
     const uint32_t a = na, id = nid;
     uint32_t pat = npat;
-    if (r + 1 < tail0) ar += nst;
-    na = cs.w0[ar];
+    if (r + 1 < tail0) {
+      ar += nst;
+      rr += rstep;
+      rn++;
+    }
+    na = rb[rr];
     npat = cs.w1[ar];
+    npat = fresh ? 0u : npat;
     if (pack) nid = cs.id[ar];
+    nid = fresh ? rn : nid;
     if (!(a & kCarEmpty)) {
       const int x = (int)(a & 255u), y = (int)((a >> 8) & 255u), prof = (int)((a >> 21) & 7u);
       int route = (int)((a >> 16) & 31u), delay = (int)((a >> 24) & 3u);
@@ -1854,7 +1871,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       if (leaves) {  // the car's square loses it
         if (sat && occ_get(occ, s_old) >= kOccMax) {
           // exact recount from HBM (this car's slot still holds its old square)
-          occ_put(occ, s_old, min(recount_slot(c, pl, cs, r, pack ? w : r, t_out, s_old), kOccMax));
+          occ_put(occ, s_old, min(recount_slot(c, pl, cs, fresh ? fb : nullptr, tail0, r, pack ? w : r, t_out, s_old), kOccMax));
         } else {
           occ_put(occ, s_old, occ_get(occ, s_old) - 1);
         }
@@ -1866,7 +1883,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
           // (two loads, not one through a selected pointer: that would be a flat load, whose wait
           // covers the LDS counter and the slot prefetch)
           uint32_t code = sp[r3 < (uint64_t)kSpCache ? r3 : 0];
-          if (r3 >= (uint64_t)kSpCache) code = ((const __attribute__((address_space(1))) uint16_t*)S.spawners)[r3 * S.n + i];
+          if (r3 >= (uint64_t)kSpCache) code = ((const __attribute__((address_space(1))) uint16_t*)S.spawners)[i * (uint64_t)S.sp_pitch + r3];
           sx = (int)(code & 255u);
           sy = (int)(code >> 8);
         }
@@ -1912,6 +1929,8 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
           cs.id[ao] = id;
           ap += nst;
           w++;
+        } else if (fresh) {
+          cs.id[ao] = id;  // (a slot row's ids are written only by the lanes of fresh envs)
         }
       }
     }
@@ -1929,6 +1948,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
     t_out = w + (t_out - tail0);
   }
   ts.tail = (uint32_t)t_out;
+  ts.fresh = 0u;  // every car is in the slot rows now
   return 0;
 }
 
@@ -2286,7 +2306,13 @@ __device__ __forceinline__ void write_obs(uint8_t* __restrict__ dst, uint32_t cn
       const uint32_t w = (uint32_t)r >> 5;
       const uint64_t two = (uint64_t)st[w] | ((uint64_t)st[w + 1] << 32);
       const uint32_t bits = (uint32_t)(two >> (r & 31));
+#ifdef PGTG_NT_OBS  // A/B: streaming (nontemporal) observation stores
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      v4u o = {expand4(bits), expand4(bits >> 4), expand4(bits >> 8), expand4(bits >> 12)};
+      __builtin_nontemporal_store(o, reinterpret_cast<v4u*>(cp));
+#else
       *reinterpret_cast<uint4*>(cp) = make_uint4(expand4(bits), expand4(bits >> 4), expand4(bits >> 8), expand4(bits >> 12));
+#endif
     } else {
       for (int b = 0; b < 16; b++) {
         const int rb = r + b;
@@ -2509,19 +2535,23 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       ts.n_spawners = tr4.x >> 16;
       ts.next_id = tr4.y;
       ts.tail = tr4.z;
-      occ_valid = tr4.w == 1u;
+      ts.fresh = (tr4.w & kTrafFresh) ? 1u : 0u;
+      occ_valid = (tr4.w & kTrafOccValid) != 0u;
     }
     stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, L.plan_stride_dw);
   }
   for (int k = tid; k < L.lm_words; k += kBlock) lm[k] = 0u;
   lds_barrier();  // sT ready
   if (live && (TR && c.need_car) && occ_valid) {
-    // the counters the last launch (or k_traffic) left: one coalesced row per counter word
+    // the counters the last launch left (one coalesced row per counter word), or k_traffic in the
+    // staging block of a fresh env
     const int nw = c.nt * 4;
+    const gu32* ob = ts.fresh ? fresh_block(S, i) + S.fresh_occ : (const gu32*)(S.occ + i);
+    const uint64_t ostep = ts.fresh ? 1ull : S.n;
     for (int w0 = 0; w0 < nw; w0 += 16) {
       uint32_t r[16];
 #pragma unroll
-      for (int u = 0; u < 16; u++) r[u] = S.occ[(uint64_t)min(w0 + u, nw - 1) * S.n + i];
+      for (int u = 0; u < 16; u++) r[u] = ob[(uint64_t)min(w0 + u, nw - 1) * ostep];
 #pragma unroll
       for (int u = 0; u < 16; u++)
         if (w0 + u < nw) traf_w[w0 + u] = r[u];
@@ -2533,16 +2563,18 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     // updated so that their HBM latency overlaps the LDS work)
     for (int w = 0; w < c.nt * 4; w++) traf_w[w] = 0u;  // 16 B of 4-bit counters per tile
     const CarSlots cs(S, i);
+    const gu32* rb = ts.fresh ? fresh_block(S, i) : cs.w0;  // (a fresh env's cars: its staging block)
+    const uint64_t rstep = ts.fresh ? 1ull : S.n;
     const int tail = (int)ts.tail, tw = pinned(c.tw);
     uint32_t nx16[16];
 #pragma unroll
-    for (int g = 0; g < 16; g++) nx16[g] = cs.w0[cs.at(g < tail ? g : 0)];
+    for (int g = 0; g < 16; g++) nx16[g] = rb[(uint64_t)(g < tail ? g : 0) * rstep];
     for (int k0 = 0; k0 < tail; k0 += 16) {
       uint32_t a16[16];
 #pragma unroll
       for (int g = 0; g < 16; g++) a16[g] = nx16[g];
 #pragma unroll
-      for (int g = 0; g < 16; g++) nx16[g] = cs.w0[cs.at(k0 + 16 + g < tail ? k0 + 16 + g : 0)];
+      for (int g = 0; g < 16; g++) nx16[g] = rb[(uint64_t)(k0 + 16 + g < tail ? k0 + 16 + g : 0) * rstep];
       // the 16 slot lookups first (every slot holds valid coordinates: empty slots read as (0, 0),
       // slots past the tail as slot 0), their reads batched; then the counter updates in order
       int sl[16];
@@ -2559,14 +2591,22 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   }
   if (live && (TR && c.need_car)) {
     // the head of the spawner list (respawn positions) into LDS
+    // (the env's list is contiguous: 16-byte loads, all issued before the LDS stores)
     const int nsp = min((int)ts.n_spawners, kSpCache);
-    for (int k0 = 0; k0 < nsp; k0 += 8) {
-      uint16_t s8[8];
+    const uint4* src = reinterpret_cast<const uint4*>(S.spawners + i * (uint64_t)S.sp_pitch);
+    const int q_last = (int)(S.sp_pitch / 8u) - 1;
+    uint4 q4[kSpCache / 8];
 #pragma unroll
-      for (int g = 0; g < 8; g++) s8[g] = S.spawners[(uint64_t)(k0 + g < nsp ? k0 + g : 0) * S.n + i];
+    for (int q = 0; q < kSpCache / 8; q++) q4[q] = src[min(q, q_last)];
+    uint32_t* dl = reinterpret_cast<uint32_t*>(sp_l);
 #pragma unroll
-      for (int g = 0; g < 8; g++)
-        if (k0 + g < nsp) sp_l[k0 + g] = s8[g];
+    for (int q = 0; q < kSpCache / 8; q++) {
+      if (q * 8 < nsp) {
+        dl[4 * q] = q4[q].x;
+        dl[4 * q + 1] = q4[q].y;
+        dl[4 * q + 2] = q4[q].z;
+        dl[4 * q + 3] = q4[q].w;
+      }
     }
   }
   STAMP(1);
@@ -2710,7 +2750,8 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       rec_store(S.rec, i, v);
       // (a reset env's counters come from k_traffic with its fresh cars; until then invalid)
       if ((TR && c.need_car))
-        S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.tail, occ_valid && !reset_now ? 1u : 0u);
+        S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.tail,
+                               (occ_valid && !reset_now ? kTrafOccValid : 0u) | (ts.fresh ? kTrafFresh : 0u));
     }
     if (mode != MODE_OBSERVE || err) S.err[i] = (uint8_t)(-err);
     if (S.qstate && reset_now) S.qstate[i] = 0;  // maps generated here: the queued ones are stale
@@ -3207,7 +3248,7 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
     if (err0 == 0) store_initial_counters(c, S, i, pl, rs, k0, sub, g);
     if (sub == 0) {
       stream_store_state(S.car, i, cr);
-      S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.tail, err == 0 ? 1u : 0u);
+      S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.tail, err == 0 ? kTrafOccValid | kTrafFresh : 0u);
       if (err) S.err[i] = (uint8_t)(-err);
       if (c.obs_fast && c.traffic_ch >= 0 && out.obs) {
         // the tile window's traffic channel: k_env wrote it with no cars; set the car squares
@@ -3313,14 +3354,18 @@ __global__ void __launch_bounds__(256) k_car_digest(DevState S, uint64_t* __rest
   constexpr uint64_t CB = 1ull << 40;
   const uint4 t = S.traf[i];
   const CarSlots cs(S, i);
+  const bool fresh = (t.w & kTrafFresh) != 0u;
+  const gu32* fb = fresh_block(S, i);
   uint64_t d = (uint64_t)(t.x & 0xffffu) * dg_w(CB), j = 0;
   for (int k = 0; k < (int)t.z; k++) {
-    const uint32_t w0 = cs.w0[cs.at(k)];
+    const uint32_t w0 = fresh ? fb[k] : cs.w0[cs.at(k)];
     if (w0 & kCarEmpty) continue;
-    const uint64_t pk = (uint64_t)cs.id[cs.at(k)] | (uint64_t)(w0 & 255u) << 32 | (uint64_t)((w0 >> 8) & 255u) << 40 |
+    const uint32_t id = fresh ? (uint32_t)k : cs.id[cs.at(k)];
+    const uint64_t pk = (uint64_t)id | (uint64_t)(w0 & 255u) << 32 | (uint64_t)((w0 >> 8) & 255u) << 40 |
                         (uint64_t)((w0 >> 16) & 31u) << 48 | (uint64_t)((w0 >> 21) & 7u) << 53 |
                         (uint64_t)((w0 >> 24) & 3u) << 56;
-    d += (pk + 1) * dg_w(CB + 1 + 2 * j) + (uint64_t)cs.w1[cs.at(k)] * dg_w(CB + 2 + 2 * j);
+    const uint32_t w1 = fresh ? 0u : cs.w1[cs.at(k)];
+    d += (pk + 1) * dg_w(CB + 1 + 2 * j) + (uint64_t)w1 * dg_w(CB + 2 + 2 * j);
     j++;
   }
   out[i] = d;
@@ -3889,10 +3934,14 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
   if (c.need_car) {
     ALLOC(S.car_w0, (uint64_t)c.car_slots * n);
     ALLOC(S.car_w1, (uint64_t)c.car_slots * n);
+    S.sp_pitch = (uint32_t)((c.max_spawners + 7) & ~7);
+    S.fresh_occ = (uint32_t)((c.car_cap + 3) & ~3);
+    S.fresh_dw = S.fresh_occ + (uint32_t)c.nt * 4u;
     ALLOC(S.car_id, (uint64_t)c.car_slots * n);
     ALLOC(S.traf, n);
     ALLOC(S.occ, (uint64_t)c.nt * 4 * n);
-    ALLOC(S.spawners, (uint64_t)c.max_spawners * n);
+    ALLOC(S.fresh, (uint64_t)S.fresh_dw * n);
+    ALLOC(S.spawners, (uint64_t)S.sp_pitch * n);
     ALLOC(S.tr_list, n);
     ALLOC(S.tr_count, 2);
   }
@@ -4170,10 +4219,15 @@ static int host_read_cars(pgtg_handle* h, uint64_t env, const uint4& t, std::vec
   const int tail = (int)t.z;
   if (tail == 0) return 0;
   const uint64_t N = h->n;
-  std::vector<uint32_t> w0(tail), w1(tail), id(tail);
-  HIPCHK(h, hipMemcpy2D(w0.data(), 4, h->S.car_w0 + env, N * 4, 4, tail, hipMemcpyDeviceToHost));
-  HIPCHK(h, hipMemcpy2D(w1.data(), 4, h->S.car_w1 + env, N * 4, 4, tail, hipMemcpyDeviceToHost));
-  HIPCHK(h, hipMemcpy2D(id.data(), 4, h->S.car_id + env, N * 4, 4, tail, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> w0(tail), w1(tail, 0u), id(tail);
+  if (t.w & kTrafFresh) {  // initial traffic still in the env's staging block (patience 0, id = slot)
+    HIPCHK(h, hipMemcpy(w0.data(), h->S.fresh + env * (uint64_t)h->S.fresh_dw, 4 * (size_t)tail, hipMemcpyDeviceToHost));
+    for (int k = 0; k < tail; k++) id[k] = (uint32_t)k;
+  } else {
+    HIPCHK(h, hipMemcpy2D(w0.data(), 4, h->S.car_w0 + env, N * 4, 4, tail, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy2D(w1.data(), 4, h->S.car_w1 + env, N * 4, 4, tail, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy2D(id.data(), 4, h->S.car_id + env, N * 4, 4, tail, hipMemcpyDeviceToHost));
+  }
   for (int k = 0; k < tail; k++) {
     if (w0[k] & kCarEmpty) continue;
     cars.push_back(PgtgCar{(int32_t)id[k], (int32_t)(w0[k] & 255u), (int32_t)((w0[k] >> 8) & 255u),
@@ -4206,7 +4260,7 @@ static int host_write_cars(pgtg_handle* h, uint64_t env, uint4 t, const std::vec
   t.x = (t.x & 0xffff0000u) | (uint32_t)n;
   t.y = next_id;
   t.z = (uint32_t)n;
-  t.w = 0u;  // the persisted occupancy counters no longer match: the next launch rebuilds them
+  t.w = 0u;  // the slot rows hold the list (not fresh); the counters no longer match: rebuilt next launch
   HIPCHK(h, hipMemcpy(h->S.traf + env, &t, sizeof t, hipMemcpyHostToDevice));
   return 0;
 }
@@ -4360,7 +4414,7 @@ struct PgtgSectionEntry {
   uint32_t id, pad;
   uint64_t bytes;
 };
-constexpr uint32_t kStateVersion = 3;
+constexpr uint32_t kStateVersion = 4;
 uint64_t cfg_hash(const DevCfg& c) {  // DevCfg is zero-initialised (derive_cfg), so padding hashes as 0
   const uint8_t* p = reinterpret_cast<const uint8_t*>(&c);
   uint64_t h = 0xcbf29ce484222325ull;
@@ -4396,7 +4450,8 @@ static std::vector<StateSection> state_sections(pgtg_handle* h) {
   add(33, S.car_id, (uint64_t)c.car_slots * n * 4);
   add(34, S.traf, n * sizeof(uint4));
   add(36, S.occ, (uint64_t)c.nt * 4 * n * 4);
-  add(35, S.spawners, (uint64_t)c.max_spawners * n * 2);
+  add(35, S.spawners, (uint64_t)S.sp_pitch * n * 2);
+  add(37, S.fresh, (uint64_t)S.fresh_dw * n * 4);
   add(40, S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw * 4);
   add(41, S.qstate, n);
   return v;

@@ -263,18 +263,32 @@ def test_step_many_equals_step_loop(name):
 
 
 def test_persisted_occupancy_counters_match_cars():
-    """DevState::occ (blob section 36) holds, for every traffic env whose traf.w flag is set, the 4-bit
-    lane-square counters of its current cars (k_env loads them instead of rebuilding them from the car
-    slots): per tile, the nibble sum equals the env's cars on that tile.  k_traffic writes them for fresh
-    traffic and k_env after every unsaturated step; set_to_state clears the flag."""
+    """The persisted 4-bit lane-square counters match the env's current cars: per tile, the nibble sum
+    equals the env's cars on that tile.  traf.w bit 0 = counters exact; bit 1 = fresh traffic, whose
+    cars and counters k_traffic wrote to the env's contiguous staging block (blob section 37: w0 of the
+    cars, then the counters at fresh_occ), else the counters are DevState::occ's slot-major rows
+    (section 36, written by k_env after every unsaturated step).  k_env loads them instead of
+    rebuilding them from the car slots; a host car write (add_car / set_to_state) clears the flags."""
     from pgtg_amd.vector import PGTGVecEnv
     spec = _spec(CONFIGS["traffic"])
     n, tw, th = 3000, 4, 4
+    nw = tw * th * 4
     env = PGTGVecEnv(n, spec=spec, device=0)
+
+    def counters(sec, i, flags):
+        if flags & 2:  # fresh: the staging block
+            blk = sec[37][0].view(np.uint32).reshape(n, -1)
+            fresh_occ = blk.shape[1] - nw
+            words = blk[i, fresh_occ:]
+        else:
+            words = sec[36][0].view(np.uint32).reshape(nw, n)[:, i]
+        words = words.reshape(tw * th, 4)
+        return sum(((words >> (4 * b)) & 15).sum(axis=1) for b in range(8))
+
     try:
         env.reset(seed=5)
         acts = env.random_actions(9, 0x0CC)
-        checked = 0
+        checked, fresh_seen = 0, 0
         for t in range(9):
             env.step_actions(acts[t])
             if t not in (0, 8):
@@ -282,17 +296,16 @@ def test_persisted_occupancy_counters_match_cars():
             blob = env.dump_state()
             sec = _sections(blob, blob)
             traf = sec[34][0].view(np.uint32).reshape(n, 4)
-            occ = sec[36][0].view(np.uint32).reshape(tw * th * 4, n)
-            valid = np.flatnonzero(traf[:, 3] == 1)
+            valid = np.flatnonzero(traf[:, 3] & 1)
             assert valid.size > n // 2, f"t{t}: only {valid.size} envs with persisted counters"
+            fresh_seen += int(((traf[:, 3] & 2) != 0).sum())
             for i in valid[:: max(1, valid.size // 200)]:
-                words = occ[:, i].reshape(tw * th, 4)
-                nib = sum(((words >> (4 * b)) & 15).sum(axis=1) for b in range(8))
+                nib = counters(sec, int(i), int(traf[i, 3]))
                 cars = env.cars(int(i))
                 per_tile = np.bincount((cars[:, 2] // 9) * tw + cars[:, 1] // 9, minlength=tw * th)
                 assert np.array_equal(nib, per_tile), f"t{t} env {i}: counters {nib} vs cars {per_tile}"
                 checked += 1
-        assert checked > 300
+        assert checked > 300 and fresh_seen > 0
         # a host car write (add_car / set_to_state) invalidates the env's counters; the next step
         # rebuilds them and persists them again
         c0 = env.cars(0)
@@ -302,10 +315,10 @@ def test_persisted_occupancy_counters_match_cars():
         env.step_actions(env.random_actions(1, 0x0CD)[0])
         blob = env.dump_state()
         sec = _sections(blob, blob)
-        if sec[34][0].view(np.uint32).reshape(n, 4)[0, 3] == 1:
-            words = sec[36][0].view(np.uint32).reshape(tw * th * 4, n)[:, 0].reshape(tw * th, 4)
-            nib = sum(((words >> (4 * b)) & 15).sum(axis=1) for b in range(8))
+        f0 = int(sec[34][0].view(np.uint32).reshape(n, 4)[0, 3])
+        if f0 & 1:
             cars = env.cars(0)
-            assert np.array_equal(nib, np.bincount((cars[:, 2] // 9) * tw + cars[:, 1] // 9, minlength=tw * th))
+            assert np.array_equal(counters(sec, 0, f0), np.bincount((cars[:, 2] // 9) * tw + cars[:, 1] // 9,
+                                                                    minlength=tw * th))
     finally:
         env.close()

@@ -84,8 +84,8 @@ for S in "$@"; do
       R=${S#pmc:}; W=${R%%:*}; L=${R#*:}; N=$(basename $L .so)
       D=$O/pmc_${W}_$N
       if [ $L = new ]; then unset PGTG_LIB; else export PGTG_LIB=$PWD/$L; fi
-      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $D/fetch -o run --output-format csv -- python bench.py --workload $W --steps 40 --warmup 10 --no-cpu-baseline > /dev/null 2>$D.err || { tail $D.err; exit 1; }
-      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $D/write -o run --output-format csv -- python bench.py --workload $W --steps 40 --warmup 10 --no-cpu-baseline > /dev/null 2>>$D.err || { tail $D.err; exit 1; }
+      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $D/fetch -o run --output-format csv -- python bench.py --workload $W --steps 60 --warmup 200 --no-cpu-baseline > /dev/null 2>$D.err || { tail $D.err; exit 1; }
+      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $D/write -o run --output-format csv -- python bench.py --workload $W --steps 60 --warmup 200 --no-cpu-baseline > /dev/null 2>>$D.err || { tail $D.err; exit 1; }
       unset PGTG_LIB
       python tools/pmc.py $W $D/fetch $D/write $N > $D.json || exit 1
       python -c "import json; d=json.load(open('$D.json')); print('$W $N', {k: round((v['read_bytes']+v['write_bytes'])/1e6,1) for k,v in d.items() if isinstance(v,dict)}, round(d['hbm_bytes_per_launch']/1e6,1), 'MB/launch')" ;;
