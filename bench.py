@@ -134,6 +134,34 @@ def load_issue(workload: str, n_envs: int, avg_kernel_s: float):
             "kernels": sorted(d["kernels"]), "source": p}
 
 
+# the stamps count shader cycles (s_memtime) at the
+# engine clock, 2.4 GHz (MI355X_MICROARCH.md)
+ENGINE_GHZ = 2.4
+
+
+def load_latency(workload: str, n_envs: int, avg_kernel_s: float):
+    """Latency bound for the launches whose workgroups are a single round of long serial chains (the
+    configs[1] batch: 16 envs per workgroup, one workgroup per CU): the measured per-wave chain of the
+    step kernel (profiles/stamps_<workload>.json, tools/stamps.py on the -DPGTG_STAMPS build) at the
+    engine clock against the measured launch duration.  frac = chain time / launch time: 1.0 means the
+    launch is exactly one wave's chain long, so only a shorter chain makes it faster."""
+    p = os.path.join("profiles", f"stamps_{workload}.json")
+    try:
+        with open(os.path.join(ROOT, p)) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("envs") != n_envs or avg_kernel_s <= 0:
+        return None
+    chain_us = d["wave_chain_cycles_mean"] / (ENGINE_GHZ * 1e3)
+    chain_max_us = d["wave_chain_cycles_max"] / (ENGINE_GHZ * 1e3)
+    return {"bound": "latency", "unit": "us", "chain_cycles_mean": d["wave_chain_cycles_mean"],
+            "chain_cycles_max": d["wave_chain_cycles_max"], "engine_ghz": ENGINE_GHZ, "chain_us_mean": chain_us,
+            "chain_us_max": chain_max_us, "avg_kernel_us": avg_kernel_s * 1e6,
+            "frac": chain_us / (avg_kernel_s * 1e6), "frac_max": chain_max_us / (avg_kernel_s * 1e6),
+            "phases_mean_cycles": d.get("phases_mean_cycles"), "source": p}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -301,6 +329,9 @@ def main():
         issue = load_issue(args.workload, n_local, avg_kernel_s)
         if issue is not None:
             rec["roofline_issue"] = issue
+        lat = load_latency(args.workload, n_local, avg_kernel_s)
+        if lat is not None:
+            rec["roofline_latency"] = lat
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)
         print(json.dumps(rec), flush=True)

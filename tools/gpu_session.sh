@@ -14,7 +14,9 @@
 #   shards           single-process lines at the per-rank shards of N = 2, 4, 8 (524 288 / 262 144 /
 #                    131 072 envs) beside the 1 048 576-env line
 #   profile:<wl,..>  tools/gpu_profile.sh (rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes)
+#   genbench         map-generation latency per map (tools/genbench.py, stamps build)
 #   stamps:<wl,..>   per-phase cycle stamps (PGTG_STAMPS build, tools/stamps.py)
+#   stampsjson:<wl> the latency record bench.py reads (copy gpurun_out/<tag>/stamps_<wl>.json to profiles/)
 #   stampslib:<lib>:<wl>  the same with a prebuilt stamps library
 #   ab:<wl>:<lib>    interleaved bench lines of the in-tree library and <lib> (tools/ab_multi.sh, 3 reps)
 #   libtests:<lib>:<expr>  pytest -m gpu -k <expr> against another build of the library (PGTG_LIB)
@@ -68,10 +70,17 @@ for S in "$@"; do
     profile:*)
       timeout -k 10 1500 bash tools/gpu_profile.sh $TAG ${S#profile:} > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
       tail -5 $O/profile.log ;;
+    genbench)
+      timeout -k 10 120 python tools/genbench.py 5 1024 8 > $O/genbench.log 2>&1 || { tail -20 $O/genbench.log; exit 1; }
+      tail -1 $O/genbench.log ;;
     stamps:*)
       python -c "from pgtg_amd.build import build; build(variant='stamps')" || exit 1
       timeout -k 10 300 python tools/stamps.py ${S#stamps:} > $O/stamps.log 2>&1 || { tail -20 $O/stamps.log; exit 1; }
       cat $O/stamps.log ;;
+    stampsjson:*)
+      W=${S#stampsjson:}
+      PGTG_STAMPS_JSON=$O/stamps_$W.json PGTG_STAMPS_WL=$W timeout -k 10 300 python tools/stamps.py $W > $O/stampsjson_$W.log 2>&1 || { tail -20 $O/stampsjson_$W.log; exit 1; }
+      cat $O/stamps_$W.json ;;
     stampslib:*)
       R=${S#stampslib:}; L=${R%%:*}; W=${R#*:}
       PGTG_STAMPS_LIB=$PWD/$L timeout -k 10 300 python tools/stamps.py $W > $O/stamps_$(basename $L .so).log 2>&1 || { tail -20 $O/stamps_$(basename $L .so).log; exit 1; }

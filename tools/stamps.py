@@ -61,10 +61,27 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
               f"(max {int((sh[okh, 7] - sh[okh, 1]).max())}), start {int((sh[okh, 1] - sh[okh, 0]).mean())}; "
               f"generate {int((sh[okh, 10] - sh[okh, 9]).mean()) if False else int((sh[okh, 15] - sh[okh, 14]).mean())} "
               f"(removal, last fill)", flush=True)
+        seg = lambda a, b: int((sh[okh, b] - sh[okh, a]).mean())  # noqa: E731
+        print(f"  helper fill (last): start/goal {seg(1, 13)} (incl. seed pool, child stream), removal {seg(14, 15)} "
+              f"(iterations {round(float(sh[okh, 27].mean()), 1)}, max {int(sh[okh, 27].max())}; connectivity tests "
+              f"{int(sh[okh, 26].mean())} cycles), borders+obstacles+masks {seg(15, 24)}, path bfs {seg(24, 25)}, "
+              f"walk+start+entry {seg(25, 7)}", flush=True)
     st = st[active]
     d = np.diff(st[:, :7], axis=1)
     print(f"{name}: {N} envs, {E} envs/workgroup, LDS {lds} B; cycles per active wave (last launch)", flush=True)
     print("  phases:", {n: int(x) for n, x in zip(PHASES, d.mean(0))}, "total", int((st[:, 6] - st[:, 0]).mean()))
+    if os.environ.get("PGTG_STAMPS_JSON"):  # the latency record bench.py reads (profiles/stamps_<workload>.json)
+        import json
+        tot = st[:, 6] - st[:, 0]
+        rec = {"workload": os.environ.get("PGTG_STAMPS_WL", name), "envs": N, "envs_per_workgroup": E,
+               "source": "tools/stamps.py (-DPGTG_STAMPS build, s_memtime per wave, last of 30 launches)",
+               "wave_chain_cycles_mean": int(tot.mean()), "wave_chain_cycles_p90": int(np.percentile(tot, 90)),
+               "wave_chain_cycles_max": int(tot.max()),
+               "phases_mean_cycles": {n: int(x) for n, x in zip(PHASES, d.mean(0))}}
+        if okh.any():
+            rec["helper_fill_cycles_mean"] = int((sh[okh, 7] - sh[okh, 1]).mean())
+        with open(os.environ["PGTG_STAMPS_JSON"], "w") as f:
+            json.dump(rec, f, indent=1)
     print("  phase p90/max:", {n: (int(np.percentile(d[:, k], 90)), int(d[:, k].max())) for k, n in enumerate(PHASES)},
           "total max", int((st[:, 6] - st[:, 0]).max()))
     lo, hi = st[:, 0], st[:, 6]
