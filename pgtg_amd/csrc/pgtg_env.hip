@@ -145,8 +145,7 @@ struct EnvView {
   uint64_t used;
 };
 
-__device__ __forceinline__ EnvView rec_load(const EnvRec* r, uint64_t i) {
-  EnvRec e = r[i];
+__device__ __forceinline__ EnvView rec_view(const EnvRec& e) {
   EnvView v;
   v.px = (int)(int16_t)(e.a.x & 0xffffu);
   v.py = (int)(int16_t)(e.a.x >> 16);
@@ -161,6 +160,7 @@ __device__ __forceinline__ EnvView rec_load(const EnvRec* r, uint64_t i) {
   v.used = (uint64_t)e.b.z | ((uint64_t)e.b.w << 32);
   return v;
 }
+__device__ __forceinline__ EnvView rec_load(const EnvRec* r, uint64_t i) { return rec_view(r[i]); }
 __device__ __forceinline__ void rec_store(EnvRec* r, uint64_t i, const EnvView& v) {
   EnvRec e;
   e.a.x = ((uint32_t)v.px & 0xffffu) | ((uint32_t)v.py << 16);
@@ -2347,6 +2347,7 @@ struct Lds {
                        // traffic region; the agent tile's counters and the reset hand-over words in hist
   int persist;         // step launches use k_envp (persistent grid of resident workgroups, decoupled helper)
   int grid;            // k_envp: workgroups of the grid
+  int helpers;         // k_envp: map-generating waves (2: the writer wave generates too, odd tiles)
   int abl;             // diagnostic ablations (PGTG_TUNING builds only, PGTG_ABL; always 0 otherwise):
                        // k_envq bit 0 no ring refills, bit 1 no terminal-observation writes, bit 2 no
                        // observation writes (timing experiments: the results are wrong)
@@ -2385,6 +2386,7 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.img_in_traf = 0;
   l.persist = 0;
   l.grid = 0;
+  l.helpers = 1;
   l.abl = 0;
 #ifdef PGTG_TUNING  // A/B and diagnostic builds only: the product library reads no environment
   if (const char* e = getenv("PGTG_ABL")) l.abl = atoi(e);
@@ -2413,7 +2415,9 @@ __host__ inline void lds_tail(Lds& l, const DevCfg& c) {
 }
 // k_envp's request ring: after the helper scratch (8-byte aligned), two slots of req_slot_dw words and
 // four flag words
-__host__ __device__ inline int req_offset(const Lds& l) { return (l.gen_off + kQueueLanes * l.plan_stride_dw + 1) & ~1; }
+__host__ __device__ inline int req_offset(const Lds& l) {
+  return (l.gen_off + (l.persist ? l.helpers : 1) * kQueueLanes * l.plan_stride_dw + 1) & ~1;
+}
 __host__ __device__ inline int req_slot_dw(const Lds& l) { return 2 * 3 * kQueueDepth + 2 * l.envs; }
 __host__ inline size_t lds_bytes(const Lds& l) {
   if (l.persist) return (size_t)4 * (req_offset(l) + 2 * req_slot_dw(l) + 4);
@@ -3184,12 +3188,16 @@ __global__ void __launch_bounds__(kBlock, 4) k_envp(const DevCfg* __restrict__ c
   }
   lds_barrier();  // tables, counter, flags
 
-  if (wave == gen_wave) {
-    // ---- helper: the refills of every tile of this workgroup, in tile order ----
-    uint16_t* gplan = reinterpret_cast<uint16_t*>(lds + L.gen_off + lane * pdw);
+  const int n_help = L.helpers;
+  if (wave >= gen_wave && wave < gen_wave + n_help) {
+    // ---- helper(s): the refills of every tile of this workgroup, in tile order (with two helpers,
+    // helper h takes the tiles of request slot h) ----
+    const int hidx = wave - gen_wave;
+    uint16_t* gplan = reinterpret_cast<uint16_t*>(lds + L.gen_off + (hidx * kQueueLanes + lane) * pdw);
     uint32_t k = 0;
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, k++) {
       const int s = (int)(k & 1u);
+      if (n_help == 2 && s != hidx) continue;
       while (__hip_atomic_load(flags + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != k + 1u)
         __builtin_amdgcn_s_sleep(2);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -3240,10 +3248,19 @@ __global__ void __launch_bounds__(kBlock, 4) k_envp(const DevCfg* __restrict__ c
   }
 
   // ---- env and writer waves ----
-  const int np = kBlock / 64 - 1;  // participating waves
-  const int rank = (wave < gen_wave ? wave : wave - 1) * 64 + lane, nthr = np * 64;
+  const int np = kBlock / 64 - n_help;  // participating waves
+  const int rank = (wave < gen_wave ? wave : wave - n_help) * 64 + lane, nthr = np * 64;
   uint32_t nbar = 0;  // sub_barrier uses so far
   uint32_t k = 0;
+  // maps of <= 64 tiles: the next tile's record, ring state, action and plan are requested before the
+  // current tile's observation writes (their latency hides behind the writes; registers are free there)
+  // (the plan goes into the env's LDS row once the writes are issued: the rows are free after the
+  // rebuild; maps of <= 32 tiles, plans of <= 4 x 16 bytes)
+  EnvRec pre_rec{};
+  uint32_t pre_qs = 0;
+  int pre_act = 0;
+  bool have_pre = false;
+  const bool pre_ok = !BIG && c.plan_stride <= 32;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, k++) {
     const int s = (int)(k & 1u);
     const uint64_t env0 = tile * (uint64_t)L.envs;
@@ -3255,10 +3272,16 @@ __global__ void __launch_bounds__(kBlock, 4) k_envp(const DevCfg* __restrict__ c
     uint32_t qs = 0;
     int act = 0;
     if (live) {
-      v = rec_load(S.rec, i);
-      qs = S.qstate[i];
-      act = actions[i];
-      stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, pdw);
+      if (have_pre) {
+        v = rec_view(pre_rec);
+        qs = pre_qs;
+        act = pre_act;
+      } else {
+        v = rec_load(S.rec, i);
+        qs = S.qstate[i];
+        act = actions[i];
+        stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, pdw);
+      }
     }
     const uint32_t qn = qs & 3u, qh = (qs >> 2) & 3u;
     for (int kk = rank; kk < L.lm_words; kk += nthr) lm[kk] = 0u;
@@ -3398,8 +3421,34 @@ __global__ void __launch_bounds__(kBlock, 4) k_envp(const DevCfg* __restrict__ c
       if (reset_now) write_small_outputs(c, out, i, v, oi, false);
     }
     sub_barrier(ctr, ++nbar * (uint32_t)np);
+    const uint64_t tn = tile + gridDim.x;
+    const uint64_t in = tn * (uint64_t)L.envs + slot;
+    const bool pre_live = pre_ok && tn < ntiles && env_wave && in < S.n;
+    uint4 pq[4];
+    if (pre_live) {  // the next tile's loads (a workgroup never has one tile twice: no overlap)
+      pre_rec = S.rec[in];
+      pre_qs = S.qstate[in];
+      pre_act = actions[in];
+      const uint4* src = reinterpret_cast<const uint4*>(S.plan + in * (uint64_t)c.plan_stride);
+      const int nq = c.plan_stride / 8;
+#pragma unroll
+      for (int kq = 0; kq < 4; kq++) pq[kq] = src[kq < nq ? kq : 0];
+    }
     if (out.obs && !(L.abl & 4))
       write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr, rank, nthr);
+    if (pre_live) {
+      const int nq = c.plan_stride / 8;
+#pragma unroll
+      for (int kq = 0; kq < 4; kq++) {
+        if (kq < nq) {
+          const uint32_t wv[4] = {pq[kq].x, pq[kq].y, pq[kq].z, pq[kq].w};
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (kq * 4 + j < pdw) plan_w[kq * 4 + j] = wv[j];
+        }
+      }
+    }
+    have_pre = pre_ok && tn < ntiles;
     if (tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
     if (k == 0u) stagger_record(L, S, t_start);  // (one tile's duration: the next launch's start ramp)
     sub_barrier(ctr, ++nbar * (uint32_t)np);  // the image, selection bytes and plan rows are free again
@@ -4146,6 +4195,9 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
     const bool on = want && per_cu >= 4 && lds_bytes(p) + kTabHead <= 40 * 1024 && blocks >= (uint64_t)2 * ncu * per_cu;
     if (on) {
       p.grid = ncu * per_cu;
+#ifdef PGTG_TUNING
+      if (const char* e = getenv("PGTG_HELPERS")) p.helpers = atoi(e) == 2 ? 2 : 1;
+#endif
       h->L = p;
     }
   }
