@@ -615,20 +615,42 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, const uint32_t* __
   // independent dependency chains per iteration); the speculative draw is rolled back on exit.
   // The next candidate's edge-table read overlaps the test; its reverse entry leaves the list at
   // the end of the iteration, before the following draw.
+#ifndef PGTG_UNIFORM_DRAW
+#define PGTG_UNIFORM_DRAW 1
+#endif
+#if PGTG_UNIFORM_DRAW
+  // the draws through a HalfStream primed every other draw (uniform: every lane is in the same
+  // iteration), so the LCG steps of all lanes fall on the same iterations
+  HalfStream hs;
+  hs.init(r);
+  hs.prime();
+  auto draw_edge = [&](int n) {
+    const int k = (int)hs.draw_int((uint32_t)n);  // n >= 2: always draws
+    const int e = L.select(k);
+    L.clear(e);
+    return e;
+  };
+#else
   auto draw_edge = [&](int n) {
     const int k = (int)pcg_draw(r, true, (uint32_t)n);  // n >= 2: always draws
     const int e = L.select(k);
     L.clear(e);
     return e;
   };
+#endif
   uint32_t pk = epk[draw_edge(nrem)];
   L.clear((int)(pk >> 17));
   nrem -= 2;
 #ifdef PGTG_STAMPS
   unsigned long long dbg_bfs = 0, dbg_iters = 0;
 #endif
-  for (;;) {
+  for (int it = 0;; it++) {
+#if PGTG_UNIFORM_DRAW
+    const HalfStream hs_before = hs;
+    if (it & 1) hs.prime();  // (draws so far: it + 1; every lane holds >= 1 half at even it)
+#else
     Pcg r_before = r;
+#endif
     const bool more = nrem > 0;  // uniform: every lane is in the same iteration
     int e_next = 0;
     if (more) e_next = draw_edge(nrem);
@@ -660,7 +682,11 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, const uint32_t* __
     dbg_iters++;
 #endif
     if (!(count > keep && more)) {
+#if PGTG_UNIFORM_DRAW
+      r = hs_before.state();  // the reference stops drawing here
+#else
       r = r_before;  // the reference stops drawing here
+#endif
       break;
     }
     L.clear((int)(pk_next >> 17));
