@@ -20,7 +20,8 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp
 VARIANTS = {"occsat": ["-DPGTG_OCC_MAX=2"]}
 # A/B and diagnostic build (tools/*.sh): reads the PGTG_SPREAD/COMPACT/QUEUE/LINEMASK/DIAG knobs from
 # the environment; the product library reads none.  Not built by default (PGTG_LIB selects it).
-TOOL_VARIANTS = {"tuning": ["-DPGTG_TUNING"], "stamps": ["-DPGTG_STAMPS"], "ntobs": ["-DPGTG_NT_OBS"]}
+TOOL_VARIANTS = {"tuning": ["-DPGTG_TUNING"], "stamps": ["-DPGTG_STAMPS"], "ntobs": ["-DPGTG_NT_OBS"],
+                 "stampsobs": ["-DPGTG_STAMPS", "-DPGTG_STAMPS_OBS"]}
 
 
 def variant_path(name: str) -> str:

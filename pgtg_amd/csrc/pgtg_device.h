@@ -362,68 +362,6 @@ __device__ __forceinline__ uint32_t ahead_int(PcgAhead& a, uint32_t n) {
   return (uint32_t)ahead_draw(a, true, n);
 }
 
-// numpy's 32-bit draws (next_uint32 halves) for a loop in which every lane draws once per iteration
-// but the lanes' buffer parities differ: with Pcg, every iteration some lanes step the 128-bit LCG, so
-// the wave executes a step (7 v_mad_u64_u32 + 6 v_mul_lo_u32) every iteration.  Here each lane steps
-// ahead at the same iterations (prime(), called at every other draw from wave-uniform control flow:
-// afterwards every lane holds >= 2 halves), keeping the stepped output pending; the draws themselves
-// then never step (except after a rare Lemire rejection).  `g` with `buf`/`has` plus the pending output
-// hold exactly numpy's stream; state() gives the numpy state (the step ahead undone).
-struct HalfStream {
-  Pcg g;          // LCG state (stepped past `pend_out` when pend), numpy buffer in g.buf / g.has
-  uint64_t pout;  // the pending 64-bit output (after g.buf when g.has)
-  uint64_t ps_hi, ps_lo;  // g's state before the pending step
-  uint32_t pend;
-  __device__ __forceinline__ void init(const Pcg& r) {
-    g = r;
-    pend = 0u;
-    pout = 0;
-    ps_hi = ps_lo = 0;
-  }
-  __device__ __forceinline__ void prime() {  // call from wave-uniform control flow
-    if (!pend) {
-      ps_hi = g.shi;
-      ps_lo = g.slo;
-      pout = pcg_next64(g);
-      pend = 1u;
-    }
-  }
-  __device__ __forceinline__ uint32_t next32() {
-    if (g.has) {
-      g.has = 0;
-      return g.buf;
-    }
-    if (pend) {
-      pend = 0u;
-      g.has = 1;
-      g.buf = (uint32_t)(pout >> 32);
-      return (uint32_t)pout;
-    }
-    return pcg_next32(g);
-  }
-  // integers(0, n) for n >= 2 (Lemire on next_uint32, numpy's buffered_bounded_lemire_uint32)
-  __device__ __forceinline__ uint32_t draw_int(uint32_t n) {
-    uint64_t m = (uint64_t)next32() * n;
-    uint32_t left = (uint32_t)m;
-    if (left < n) {
-      const uint32_t thr = (0xffffffffu - (n - 1u)) % n;
-      while (left < thr) {
-        m = (uint64_t)next32() * n;
-        left = (uint32_t)m;
-      }
-    }
-    return (uint32_t)(m >> 32);
-  }
-  __device__ __forceinline__ Pcg state() const {  // numpy's state: the step ahead undone
-    Pcg r = g;
-    if (pend) {
-      r.shi = ps_hi;
-      r.slo = ps_lo;
-    }
-    return r;
-  }
-};
-
 // ------------------------------------------------------------------------------------------------
 // PCG64 jump-ahead.  s_{n+d} = M^d s_n + (1 + M + ... + M^(d-1)) inc, so a jump of d outputs
 // composes the jumps of d's set bits: kPcgJump[b] = {M^(2^b), G(2^b)} (hi, lo words), G(2d) = G(d)

@@ -615,42 +615,20 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, const uint32_t* __
   // independent dependency chains per iteration); the speculative draw is rolled back on exit.
   // The next candidate's edge-table read overlaps the test; its reverse entry leaves the list at
   // the end of the iteration, before the following draw.
-#ifndef PGTG_UNIFORM_DRAW
-#define PGTG_UNIFORM_DRAW 1
-#endif
-#if PGTG_UNIFORM_DRAW
-  // the draws through a HalfStream primed every other draw (uniform: every lane is in the same
-  // iteration), so the LCG steps of all lanes fall on the same iterations
-  HalfStream hs;
-  hs.init(r);
-  hs.prime();
-  auto draw_edge = [&](int n) {
-    const int k = (int)hs.draw_int((uint32_t)n);  // n >= 2: always draws
-    const int e = L.select(k);
-    L.clear(e);
-    return e;
-  };
-#else
   auto draw_edge = [&](int n) {
     const int k = (int)pcg_draw(r, true, (uint32_t)n);  // n >= 2: always draws
     const int e = L.select(k);
     L.clear(e);
     return e;
   };
-#endif
   uint32_t pk = epk[draw_edge(nrem)];
   L.clear((int)(pk >> 17));
   nrem -= 2;
 #ifdef PGTG_STAMPS
   unsigned long long dbg_bfs = 0, dbg_iters = 0;
 #endif
-  for (int it = 0;; it++) {
-#if PGTG_UNIFORM_DRAW
-    const HalfStream hs_before = hs;
-    if (it & 1) hs.prime();  // (draws so far: it + 1; every lane holds >= 1 half at even it)
-#else
+  for (;;) {
     Pcg r_before = r;
-#endif
     const bool more = nrem > 0;  // uniform: every lane is in the same iteration
     int e_next = 0;
     if (more) e_next = draw_edge(nrem);
@@ -682,11 +660,7 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, const uint32_t* __
     dbg_iters++;
 #endif
     if (!(count > keep && more)) {
-#if PGTG_UNIFORM_DRAW
-      r = hs_before.state();  // the reference stops drawing here
-#else
       r = r_before;  // the reference stops drawing here
-#endif
       break;
     }
     L.clear((int)(pk_next >> 17));
@@ -1574,6 +1548,9 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
                                           uint32_t* img, uint32_t bit0, ObsInfo& oi, const uint8_t* occ,
                                           int ch_lo = 0, int ch_hi = -1, bool head = true, bool lane_codes = false,
                                           bool occ_tile_only = false) {  // occ: the agent tile's 16 bytes only
+#ifdef PGTG_STAMPS_OBS  // diagnostic: build_obs's setup (k_envq env waves only: slots 9-11 are free there)
+  STAMP(9);
+#endif
   const int WW = c.win * c.win;
   if (ch_hi < 0) ch_hi = c.n_channels;
   BitSink sink(img, bit0 + (uint32_t)(ch_lo * WW));
@@ -1593,8 +1570,15 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
   if (!c.sliding && !c.generic_channels) {
     // fast path: the window is exactly one tile -> 81-bit table algebra
     int t = ty * c.tw + tx;
+#ifdef PGTG_STAMPS_OBS
+    STAMP(10);
+#endif
     uint32_t p = pl[t];
     uint32_t ex = plan_exits(p);
+#ifdef PGTG_STAMPS_OBS
+    if (ex == 99u) ex = 0u;  // (forces the plan read before the stamp below)
+    STAMP(11);
+#endif
     uint32_t W3[3], SG[3] = {0, 0, 0}, US[3] = {0, 0, 0}, FI[3] = {0, 0, 0}, ST[3] = {0, 0, 0}, OB[3] = {0, 0, 0};
     int sd = plan_sgdir(p);
     bool used = used_bit<BIG>(v, p, t);
@@ -2371,9 +2355,6 @@ struct Lds {
   int stagger_wgs;     // workgroups resident in the first round (blocks per CU x CUs)
   int img_in_traf;     // k_env with traffic: the whole workgroup's image in the (after the car pass dead)
                        // traffic region; the agent tile's counters and the reset hand-over words in hist
-  int persist;         // step launches use k_envp (persistent grid of resident workgroups, decoupled helper)
-  int grid;            // k_envp: workgroups of the grid
-  int helpers;         // k_envp: map-generating waves (2: the writer wave generates too, odd tiles)
   int abl;             // diagnostic ablations (PGTG_TUNING builds only, PGTG_ABL; always 0 otherwise):
                        // k_envq bit 0 no ring refills, bit 1 no terminal-observation writes, bit 2 no
                        // observation writes (timing experiments: the results are wrong)
@@ -2381,7 +2362,6 @@ struct Lds {
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
 constexpr uint64_t kStaggerMaxTicks = 20000;  // 200 us of 100 MHz wall clock: a bound, never reached
 constexpr int kQueueDepth = 3;   // queued maps per env (a ring)
-constexpr bool kPersistDefault = false;  // k_envp for multi-round map-queue launches (A/B: PGTG_PERSIST)
 
 __host__ __device__ inline int odd_up(int x) { return x | 1; }
 // words of a dense observation image of `envs` envs (+2: the writers' funnel reads run one word
@@ -2410,9 +2390,6 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.stagger = 0;
   l.stagger_wgs = 0;
   l.img_in_traf = 0;
-  l.persist = 0;
-  l.grid = 0;
-  l.helpers = 1;
   l.abl = 0;
 #ifdef PGTG_TUNING  // A/B and diagnostic builds only: the product library reads no environment
   if (const char* e = getenv("PGTG_ABL")) l.abl = atoi(e);
@@ -2439,14 +2416,7 @@ __host__ inline void lds_tail(Lds& l, const DevCfg& c) {
   l.gen_off = (int)(((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
                     tail_bytes(l) / 4);
 }
-// k_envp's request ring: after the helper scratch (8-byte aligned), two slots of req_slot_dw words and
-// four flag words
-__host__ __device__ inline int req_offset(const Lds& l) {
-  return (l.gen_off + (l.persist ? l.helpers : 1) * kQueueLanes * l.plan_stride_dw + 1) & ~1;
-}
-__host__ __device__ inline int req_slot_dw(const Lds& l) { return 2 * 3 * kQueueDepth + 2 * l.envs; }
 __host__ inline size_t lds_bytes(const Lds& l) {
-  if (l.persist) return (size_t)4 * (req_offset(l) + 2 * req_slot_dw(l) + 4);
   return (size_t)4 * ((size_t)l.envs * (l.plan_stride_dw + l.scratch_dw + l.traf_dw + l.hist_dw) + l.stream_words) +
          tail_bytes(l) + (l.queue ? (size_t)4 * kQueueLanes * l.plan_stride_dw : 0);
 }
@@ -3173,314 +3143,6 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   STAMP(6);
 }
 
-// Persistent form of k_envq for launches of several rounds of workgroups: one resident grid whose
-// workgroups step tiles blockIdx.x, blockIdx.x + gridDim.x, ... (128 envs each), and whose helper wave
-// runs decoupled from the env waves.  In k_envq every workgroup's time is the slower of its env waves'
-// chain and its helper's one map generation, and a round's tables, plans and records are staged anew.
-// Here the env waves hand each tile's refill list (masks, spawn counters, ring states) to the helper
-// through a two-slot request ring in LDS and go on with the tile; the helper generates the refills of
-// tile k while the env waves work on tile k or k + 1, so per tile the two chains average instead of
-// adding their spreads.  Only a tile with an empty ring at launch start (qn == 0: after a reset
-// without the ring fill, or a refill backlog) waits for the helper's head refills of that tile before
-// the resets take their ring heads.  Same results as k_envq (the same refill lists and ring-state
-// bookkeeping).
-template <bool BIG>
-__global__ void __launch_bounds__(kBlock, 4) k_envp(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
-                                                    DevState S, const uint8_t* __restrict__ actions, PgtgOutputs out,
-                                                    Lds L) {
-  extern __shared__ uint32_t lds[];
-  const DevCfg& c = *cfg;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint64_t t_start = stagger_start(L, S);
-  stage_tables(gtab, false);
-  const int env_waves = (L.envs + 63) / 64, gen_wave = env_waves;
-  const bool env_wave = wave < env_waves;
-  const int slot = tid;
-  const int pdw = L.plan_stride_dw;
-  uint32_t* plan_w = lds + (env_wave ? slot : 0) * pdw;
-  uint32_t* st = lds + L.envs * (pdw + L.scratch_dw + L.traf_dw + L.hist_dw);
-  uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(sel + kBlock + 72);  // sub_barrier counter (env + writer waves)
-  uint32_t* lm = L.lm_words ? reinterpret_cast<uint32_t*>(sel + kBlock + 128) : nullptr;  // terminal lines
-  // request ring (two slots): per slot fm[level][env wave] (u64), then per env slot {spawn, ring state};
-  // flags[0..1] = tile count + 1 published into the slot, flags[2..3] = tile count + 1 the helper is done with
-  uint32_t* req = lds + req_offset(L);
-  const int kReqDw = req_slot_dw(L);  // words per slot (fm, then {spawn, ring state} pairs)
-  uint32_t* flags = req + 2 * kReqDw;
-  const uint64_t ntiles = (S.n + L.envs - 1) / L.envs;
-  if (tid == 0) {
-    *ctr = 0u;
-    flags[0] = flags[1] = flags[2] = flags[3] = 0u;
-  }
-  lds_barrier();  // tables, counter, flags
-
-  const int n_help = L.helpers;
-  if (wave >= gen_wave && wave < gen_wave + n_help) {
-    // ---- helper(s): the refills of every tile of this workgroup, in tile order (with two helpers,
-    // helper h takes the tiles of request slot h) ----
-    const int hidx = wave - gen_wave;
-    uint16_t* gplan = reinterpret_cast<uint16_t*>(lds + L.gen_off + (hidx * kQueueLanes + lane) * pdw);
-    uint32_t k = 0;
-    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, k++) {
-      const int s = (int)(k & 1u);
-      if (n_help == 2 && s != hidx) continue;
-      while (__hip_atomic_load(flags + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != k + 1u)
-        __builtin_amdgcn_s_sleep(2);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-      const uint64_t* fm = reinterpret_cast<const uint64_t*>(req + s * kReqDw);
-      const uint32_t* xq = req + s * kReqDw + 2 * 3 * kQueueDepth;
-      const uint64_t env0 = tile * (uint64_t)L.envs;
-      int F[kQueueDepth];
-#pragma unroll
-      for (int l = 0; l < kQueueDepth; l++) {
-        F[l] = 0;
-        for (int w = 0; w < env_waves; w++) F[l] += __popcll(fm[l * 3 + w]);
-      }
-      auto refill = [&](int kk, int l) {
-        int e = 0, pre = 0;
-        for (int w = 0; w < env_waves; w++) {
-          const uint64_t m = fm[l * 3 + w];
-          const int cw = __popcll(m);
-          if (kk >= pre && kk < pre + cw) e = w * 64 + select64(m, kk - pre);
-          pre += cw;
-        }
-        const uint64_t ie = env0 + e;
-        const uint32_t qe = xq[2 * e + 1];
-        const uint32_t rslot = (((qe >> 2) & 3u) + (uint32_t)l) % (uint32_t)kQueueDepth;
-        gen_queue_entry<BIG>(c, S, ie, xq[2 * e] + 5u * (uint32_t)l, gplan, pdw,
-                             S.qbuf + (ie * kQueueDepth + rslot) * (uint64_t)c.qrec_dw);
-      };
-      if (!(L.abl & 1)) {
-        for (int kk = lane; kk < F[0]; kk += kQueueLanes) refill(kk, 0);  // empty rings' heads, all of them
-        int kk = lane, l = 1;
-        while (l < kQueueDepth && kk >= F[l]) {
-          kk -= F[l];
-          l++;
-        }
-        if (l < kQueueDepth) refill(kk, l);
-      }
-      if (lane == 0) {
-        int rest = 0;
-        for (int l = 1; l < kQueueDepth; l++) rest += F[l];
-        atomicAdd(&S.counters[2], (unsigned long long)(F[0] + min(rest, kQueueLanes)));
-      }
-      // the slot's LDS data has been read: release it.  The entries' HBM stores need not be complete
-      // unless some ring of the tile was empty (the env waves then wait for its head refills)
-      if (F[0] > 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      if (lane == 0) __hip_atomic_store(flags + 2 + s, k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    return;
-  }
-
-  // ---- env and writer waves ----
-  const int np = kBlock / 64 - n_help;  // participating waves
-  const int rank = (wave < gen_wave ? wave : wave - n_help) * 64 + lane, nthr = np * 64;
-  uint32_t nbar = 0;  // sub_barrier uses so far
-  uint32_t k = 0;
-  // maps of <= 64 tiles: the next tile's record, ring state, action and plan are requested before the
-  // current tile's observation writes (their latency hides behind the writes; registers are free there)
-  // (the plan goes into the env's LDS row once the writes are issued: the rows are free after the
-  // rebuild; maps of <= 32 tiles, plans of <= 4 x 16 bytes)
-  EnvRec pre_rec{};
-  uint32_t pre_qs = 0;
-  int pre_act = 0;
-  bool have_pre = false;
-  const bool pre_ok = !BIG && c.plan_stride <= 32;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, k++) {
-    const int s = (int)(k & 1u);
-    const uint64_t env0 = tile * (uint64_t)L.envs;
-    const int nb = (int)min((uint64_t)L.envs, S.n - env0);
-    const uint64_t i = env0 + slot;
-    const bool live = env_wave && slot < nb;
-    Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
-    EnvView v{};
-    uint32_t qs = 0;
-    int act = 0;
-    if (live) {
-      if (have_pre) {
-        v = rec_view(pre_rec);
-        qs = pre_qs;
-        act = pre_act;
-      } else {
-        v = rec_load(S.rec, i);
-        qs = S.qstate[i];
-        act = actions[i];
-        stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, pdw);
-      }
-    }
-    const uint32_t qn = qs & 3u, qh = (qs >> 2) & 3u;
-    for (int kk = rank; kk < L.lm_words; kk += nthr) lm[kk] = 0u;
-    // the request slot is free once the helper is done with tile k - 2
-    if (k >= 2u)
-      while (__hip_atomic_load(flags + 2 + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != k - 1u)
-        __builtin_amdgcn_s_sleep(2);
-    uint64_t* fm = reinterpret_cast<uint64_t*>(req + s * kReqDw);
-    uint32_t* xq = req + s * kReqDw + 2 * 3 * kQueueDepth;
-    if (env_wave) {  // refills: ring level l (0 = head) for the envs holding <= l maps
-      if (live) {
-        xq[2 * slot] = v.spawn;
-        xq[2 * slot + 1] = qs;
-      }
-#pragma unroll
-      for (int l = 0; l < kQueueDepth; l++) {
-        const uint64_t m = __ballot(live && qn <= (uint32_t)l);
-        if (lane == 0) fm[l * 3 + wave] = m;
-      }
-    }
-    sub_barrier(ctr, ++nbar * (uint32_t)np);  // request slot and line mask written
-    if (tid == 0) {  // (every wave's slot writes happen-before the barrier; publish them to the helper)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      __hip_atomic_store(flags + s, k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    // (the slot stays as written until these waves write it again two tiles later: the helper only
-    // reads it, so the masks are read from it again where they are needed)
-    bool any_empty = false;
-    for (int w = 0; w < env_waves; w++) any_empty = any_empty || fm[w] != 0ull;
-
-    uint8_t my_sel = 0;
-    int err = 0;
-    if (live) {
-      StepResult res{0.0, 0.0, 0u};
-      bool occ_sat = false;
-      TrafState ts{0, 0, 0, 0};
-      err = env_step<false, BIG>(c, S, i, v, pl, act, res, nullptr, occ_sat, nullptr, ts, nullptr);
-      const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
-      if (out.reward) out.reward[i] = res.reward;
-      if (out.cost) out.cost[i] = res.cost;
-      if (out.terminated) out.terminated[i] = (v.flags & kFlagTerminated) ? 1 : 0;
-      if (out.truncated) out.truncated[i] = (v.flags & kFlagTruncated) ? 1 : 0;
-      if (out.braking) out.braking[i] = 0;
-      my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
-      if (BIG && res.plan_dirty && !my_sel) store_plan_row(c, S, i, plan_w, pdw);  // used subgoals (kPlanUsed)
-      if (lm && my_sel && out.final_obs) mark_lines(lm, out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)slot, (uint32_t)c.obs_bytes);
-    }
-    {
-      ObsInfo oi;
-      group_obs<BIG>(c, S, v, live, st, oi, L, wave, lane);
-      if (live) write_small_outputs(c, out, i, v, oi, my_sel == 1);
-    }
-    if (env_wave) sel[slot] = my_sel;
-    const uint64_t rm = __ballot(my_sel == 1);
-    if (env_wave && lane == 0 && rm) atomicAdd(&S.counters[1], (unsigned long long)__popcll(rm));
-    sub_barrier(ctr, ++nbar * (uint32_t)np);
-    if (out.final_obs && !(L.abl & 2))
-      write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, rank, nthr, lm);
-    sub_barrier(ctr, ++nbar * (uint32_t)np);  // terminal images written before they are rebuilt
-    const bool reset_now = my_sel != 0;
-    if (any_empty) {  // some ring of the tile was empty: wait for the helper's head refills of this tile
-      while (__hip_atomic_load(flags + 2 + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != k + 1u)
-        __builtin_amdgcn_s_sleep(2);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    }
-    if (reset_now) {  // the ring's head becomes the episode (env_reset without the generation)
-      const uint4* q4 = reinterpret_cast<const uint4*>(S.qbuf + (i * kQueueDepth + qh) * (uint64_t)c.qrec_dw);
-      uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
-      const int nq = c.plan_stride / 8;
-      const uint4 meta = q4[nq];
-      for (int k0 = 0; k0 < (BIG ? nq : 1); k0 += 8) {
-        uint4 qw[8];
-#pragma unroll
-        for (int kq = 0; kq < 8; kq++) qw[kq] = q4[k0 + kq < nq ? k0 + kq : k0];
-#pragma unroll
-        for (int kq = 0; kq < 8; kq++) {
-          if (k0 + kq < nq) {
-            dstp[k0 + kq] = qw[kq];
-            const uint32_t wv[4] = {qw[kq].x, qw[kq].y, qw[kq].z, qw[kq].w};
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-              if ((k0 + kq) * 4 + j < pdw) plan_w[(k0 + kq) * 4 + j] = wv[j];
-          }
-        }
-      }
-      const uint32_t k0s = v.spawn;
-      if (c.need_ice || c.need_broken || c.need_sand) {
-        SeedPool sp = ss_pool(S.seed[i]);
-        if (c.need_ice) stream_store_all(S.ice, i, ss_child(sp, k0s + 2u));
-        if (c.need_broken) stream_store_all(S.broken, i, ss_child(sp, k0s + 3u));
-        if (c.need_sand) stream_store_all(S.sand, i, ss_child(sp, k0s + 4u));
-      }
-      v.spawn = k0s + 5u;
-      v.sg = meta.y;
-      v.used = 0;
-      v.path_len = meta.z & 0xffffu;
-      v.flags = 0;
-      v.phase = 0;
-      v.elapsed = 0;
-      v.vx = v.vy = 0;
-      v.px = (int)(int16_t)(meta.x & 0xffffu);
-      v.py = (int)(int16_t)(meta.x >> 16);
-      const int e2 = -(int)(meta.z >> 16);
-      if (e2) err = e2;
-      if (S.visited && e2 == 0) {
-        uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
-        for (int q2 = 0; q2 < c.vis_words; q2++) vis[q2] = 0;
-        int b = (v.px + 2) * c.vis_pitch + (v.py + 2);
-        vis[b >> 5] |= 1u << (b & 31);
-      }
-    }
-    if (live) {
-      rec_store(S.rec, i, v);
-      S.err[i] = (uint8_t)(-err);
-      // ring entries after this launch: the refills served (the helper's list order) minus the head a
-      // reset took (an inline map counts as the head refill)
-      uint32_t have = qn == 0u ? 1u : qn;
-      int base = 0;
-#pragma unroll
-      for (int l = 1; l < kQueueDepth; l++) {
-        int pre = 0, fl = 0;
-        for (int w = 0; w < env_waves; w++) {
-          const int cw = __popcll(fm[l * 3 + w]);
-          pre += w < wave ? cw : 0;
-          fl += cw;
-        }
-        if (qn <= (uint32_t)l && base + pre + __popcll(fm[l * 3 + wave] & ((1ull << lane) - 1ull)) < kQueueLanes) have++;
-        base += fl;
-      }
-      const uint32_t nq = reset_now ? have - 1u : have;
-      const uint32_t nh = reset_now ? (qh + 1u) % (uint32_t)kQueueDepth : qh;
-      S.qstate[i] = (uint8_t)(nq | nh << 2);
-    }
-    {
-      ObsInfo oi;
-      group_obs<BIG>(c, S, v, reset_now, st, oi, L, wave, lane, false);
-      if (reset_now) write_small_outputs(c, out, i, v, oi, false);
-    }
-    sub_barrier(ctr, ++nbar * (uint32_t)np);
-    const uint64_t tn = tile + gridDim.x;
-    const uint64_t in = tn * (uint64_t)L.envs + slot;
-    const bool pre_live = pre_ok && tn < ntiles && env_wave && in < S.n;
-    uint4 pq[4];
-    if (pre_live) {  // the next tile's loads (a workgroup never has one tile twice: no overlap)
-      pre_rec = S.rec[in];
-      pre_qs = S.qstate[in];
-      pre_act = actions[in];
-      const uint4* src = reinterpret_cast<const uint4*>(S.plan + in * (uint64_t)c.plan_stride);
-      const int nq = c.plan_stride / 8;
-#pragma unroll
-      for (int kq = 0; kq < 4; kq++) pq[kq] = src[kq < nq ? kq : 0];
-    }
-    if (out.obs && !(L.abl & 4))
-      write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr, rank, nthr);
-    if (pre_live) {
-      const int nq = c.plan_stride / 8;
-#pragma unroll
-      for (int kq = 0; kq < 4; kq++) {
-        if (kq < nq) {
-          const uint32_t wv[4] = {pq[kq].x, pq[kq].y, pq[kq].z, pq[kq].w};
-#pragma unroll
-          for (int j = 0; j < 4; j++)
-            if (kq * 4 + j < pdw) plan_w[kq * 4 + j] = wv[j];
-        }
-      }
-    }
-    have_pre = pre_ok && tn < ntiles;
-    if (tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
-    if (k == 0u) stagger_record(L, S, t_start);  // (one tile's duration: the next launch's start ramp)
-    sub_barrier(ctr, ++nbar * (uint32_t)np);  // the image, selection bytes and plan rows are free again
-  }
-}
-
 // Fill every env's map ring (after a reset, whose k_env launch generated the current episodes' maps and
 // emptied the rings): one lane per env generates the missing entries in ring order, spawn counters
 // spawn, spawn + 5, spawn + 10 -- the maps k_envq's helper wave would generate over the first launches
@@ -3777,7 +3439,6 @@ struct pgtg_handle {
 static const void* step_fn(const pgtg_handle* h, int mode) {
   const bool big = h->hcfg.nt > kSmallTiles;
   if (h->hcfg.need_car || h->hcfg.n_rules > 0) return big ? (const void*)k_env<true, true> : (const void*)k_env<true, false>;
-  if (mode == MODE_STEP && h->L.queue && h->L.persist) return big ? (const void*)k_envp<true> : (const void*)k_envp<false>;
   if (mode == MODE_STEP && h->L.queue) return big ? (const void*)k_envq<true> : (const void*)k_envq<false>;
   return big ? (const void*)k_env<false, true> : (const void*)k_env<false, false>;
 }
@@ -4203,30 +3864,6 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
     h->L.queue = 0;
     lds_tail(h->L, c);
   }
-  // launches of two rounds of workgroups or more: the persistent grid (k_envp) instead
-  h->L.persist = 0;
-  h->L.grid = 0;
-  if (h->L.queue && h->L.envs == 128) {
-    Lds p = h->L;
-    p.persist = 1;
-    int ncu = 0, per_cu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || ncu < 1) ncu = 256;
-    const void* fn = c.nt > kSmallTiles ? (const void*)k_envp<true> : (const void*)k_envp<false>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds_bytes(p)) != hipSuccess || per_cu < 1) per_cu = 0;
-    const uint64_t blocks = (h->n + p.envs - 1) / p.envs;
-    bool want = kPersistDefault;
-#ifdef PGTG_TUNING
-    if (const char* e = getenv("PGTG_PERSIST")) want = atoi(e) != 0;
-#endif
-    const bool on = want && per_cu >= 4 && lds_bytes(p) + kTabHead <= 40 * 1024 && blocks >= (uint64_t)2 * ncu * per_cu;
-    if (on) {
-      p.grid = ncu * per_cu;
-#ifdef PGTG_TUNING
-      if (const char* e = getenv("PGTG_HELPERS")) p.helpers = atoi(e) == 2 ? 2 : 1;
-#endif
-      h->L = p;
-    }
-  }
   h->lds = lds_bytes(h->L);
   if (h->lds + sizeof(Tables) > 160 * 1024) return fail(h, PGTG_E_UNSUPPORTED, "LDS budget exceeded");
   if (h->lds > 64 * 1024) {
@@ -4452,10 +4089,7 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
   }
   const void* fn = step_fn(h, mode);
   void* args[] = {&h->dcfg, &h->dtab, &h->S, &actions, &mask, &h->out, &mode, &h->L, &h->tr_slot};
-  if (fn == (const void*)k_envp<false> || fn == (const void*)k_envp<true>) {
-    void* qargs[] = {&h->dcfg, &h->dtab, &h->S, &actions, &h->out, &h->L};
-    HIPCHK(h, hipLaunchKernel(fn, dim3((unsigned)h->L.grid), dim3(kBlock), qargs, h->lds, h->stream));
-  } else if (fn == (const void*)k_envq<false> || fn == (const void*)k_envq<true>) {
+  if (fn == (const void*)k_envq<false> || fn == (const void*)k_envq<true>) {
     void* qargs[] = {&h->dcfg, &h->dtab, &h->S, &actions, &h->out, &h->L};
     HIPCHK(h, hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(kBlock), qargs, h->lds, h->stream));
   } else {
@@ -5100,7 +4734,6 @@ const char* pgtg_step_kernel(const pgtg_handle* h) {
   const bool big = h->hcfg.nt > kSmallTiles;
   if (h->hcfg.need_car) return big ? "pgtg::k_env<true, true> + pgtg::k_traffic" : "pgtg::k_env<true, false> + pgtg::k_traffic";
   if (h->hcfg.n_rules > 0) return big ? "pgtg::k_env<true, true>" : "pgtg::k_env<true, false>";
-  if (h->L.queue && h->L.persist) return big ? "pgtg::k_envp<true>" : "pgtg::k_envp<false>";
   if (h->L.queue) return big ? "pgtg::k_envq<true>" : "pgtg::k_envq<false>";
   return big ? "pgtg::k_env<false, true>" : "pgtg::k_env<false, false>";
 }

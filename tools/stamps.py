@@ -28,6 +28,7 @@ SUB = {"cars": (16, 17), "braking": (17, 18), "reset.seed": (8, 9), "reset.gener
        "q.env_step": (1, 22), "q.outputs": (22, 23), "bo.setup": (23, 19), "bo.channels": (19, 20),
        "bo.finish_nsd": (20, 21),
        "grp.post.shfl": (9, 10), "grp.post.build": (10, 11), "grp.post.tail": (11, 2),
+       "obsdiag.enter": (23, 9), "obsdiag.scalars": (9, 10), "obsdiag.plan": (10, 11), "obsdiag.tables": (11, 19),
        "grp.rebuild.shfl": (16, 17), "grp.rebuild.build": (17, 18)}
 CASES = {"cfg2": (4096, dict(random_map_width=3, random_map_height=3)),
          "cfg5": (131072, dict(random_map_width=5, random_map_height=5)),
