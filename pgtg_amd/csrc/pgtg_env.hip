@@ -1730,12 +1730,13 @@ __device__ __forceinline__ T sel4(int k, T a0, T a1, T a2, T a3) {
 // Exact number of cars on lane slot s while the car in slot r leaves it: slots [0, w) hold the cars
 // already moved this tick (w = r, or the packed count when the tick packs), (r, tail0) those still
 // to move, [tail0, t_out) this tick's respawns.  Rare: only once a 4-bit occupancy counter saturated.
-__device__ __noinline__ int recount_slot(const DevCfg& c, const Plan& pl, const CarSlots& cs, int r, int w, int t_out,
-                                         int s) {
+// A fresh env (fw0: its staging block) still holds the cars not yet moved, (r, tail0), there.
+__device__ __noinline__ int recount_slot(const DevCfg& c, const Plan& pl, const CarSlots& cs, const gu32* fw0, int tail0,
+                                         int r, int w, int t_out, int s) {
   int n = 0;
   for (int k = 0; k < t_out; k++) {
     if (k >= w && k <= r) continue;
-    const uint32_t w0 = cs.w0[cs.at(k)];
+    const uint32_t w0 = (fw0 && k > r && k < tail0) ? fw0[k] : cs.w0[cs.at(k)];
     if (w0 & kCarEmpty) continue;
     n += lane_slot(c, pl, (int)(w0 & 255u), (int)((w0 >> 8) & 255u)) == s ? 1 : 0;
   }
@@ -1764,27 +1765,12 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
   const int tw = c.tw, th = c.th;
   const uint32_t nsp = ts.n_spawners;
   const int tail0 = (int)ts.tail;
-  if (ts.fresh) {
-    // initial traffic (k_traffic) is still in the env's staging block: into the slot rows first, with
-    // patience 0 and id = slot.  Only the lanes of fresh envs store here (a few per wave); the pass
-    // below rewrites the same w0/w1 row words while their lines are still in the L2.
-    const uint4* fb4 = reinterpret_cast<const uint4*>(S.fresh + i * (uint64_t)S.fresh_dw);
-    uint64_t a = cs.at(0);
-    for (int k0 = 0; k0 < tail0; k0 += 4) {
-      const uint4 q = fb4[k0 >> 2];
-      const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        if (k0 + u < tail0) {
-          cs.w0[a] = qw[u];
-          cs.w1[a] = 0u;
-          cs.id[a] = (uint32_t)(k0 + u);
-        }
-        a += S.n;
-      }
-    }
-    ts.fresh = 0u;
-  }
+  // a fresh env (initial traffic from k_traffic) reads its cars from its staging block, patience 0;
+  // every env writes the slot rows
+  const bool fresh = ts.fresh != 0;
+  gu32* const fb = fresh_block(S, i);
+  const gu32* const rb = fresh ? fb : cs.w0;
+  const uint64_t rstep = fresh ? 1ull : S.n;
   // (wave-uniform: packing is right for any list, and a uniform flag keeps the loop free of
   // exec-mask juggling around the packing writes)
   const bool pack = __any(tail0 > (int)ts.n_cars + kCompactSlack);
@@ -1794,17 +1780,26 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
   const uint64_t nst = S.n;
   // software pipeline: the next slot's words are requested before the current car is processed, so
   // their HBM latency overlaps this car's work (slot indices advance by the env stride)
-  uint64_t ar = cs.at(0), an = cs.at(tail0), ap = cs.at(0);
-  uint32_t na = cs.w0[ar], npat = cs.w1[ar], nid = 0u;
+  uint64_t ar = cs.at(0), an = cs.at(tail0), ap = cs.at(0), rr = 0;
+  uint32_t rn = 0;  // the prefetched slot (a fresh env's car ids are its slot indices)
+  uint32_t na = rb[rr], npat = cs.w1[ar], nid = 0u;
+  npat = fresh ? 0u : npat;
   if (pack) nid = cs.id[ar];
+  nid = fresh ? rn : nid;
   for (int r = 0; r < tail0; r++) {
     const uint64_t aw = ar;
     const uint32_t a = na, id = nid;
     uint32_t pat = npat;
-    if (r + 1 < tail0) ar += nst;
-    na = cs.w0[ar];
+    if (r + 1 < tail0) {
+      ar += nst;
+      rr += rstep;
+      rn++;
+    }
+    na = rb[rr];
     npat = cs.w1[ar];
+    npat = fresh ? 0u : npat;
     if (pack) nid = cs.id[ar];
+    nid = fresh ? rn : nid;
     if (!(a & kCarEmpty)) {
       const int x = (int)(a & 255u), y = (int)((a >> 8) & 255u), prof = (int)((a >> 21) & 7u);
       int route = (int)((a >> 16) & 31u), delay = (int)((a >> 24) & 3u);
@@ -1886,7 +1881,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
       if (leaves) {  // the car's square loses it
         if (sat && occ_get(occ, s_old) >= kOccMax) {
           // exact recount from HBM (this car's slot still holds its old square)
-          occ_put(occ, s_old, min(recount_slot(c, pl, cs, r, pack ? w : r, t_out, s_old), kOccMax));
+          occ_put(occ, s_old, min(recount_slot(c, pl, cs, fresh ? fb : nullptr, tail0, r, pack ? w : r, t_out, s_old), kOccMax));
         } else {
           occ_put(occ, s_old, occ_get(occ, s_old) - 1);
         }
@@ -1944,6 +1939,8 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
           cs.id[ao] = id;
           ap += nst;
           w++;
+        } else if (fresh) {
+          cs.id[ao] = id;  // (a slot row's ids are written only by the lanes of fresh envs)
         }
       }
     }
@@ -1961,6 +1958,7 @@ __device__ __forceinline__ int move_cars(const DevCfg& c, const DevState& S, uin
     t_out = w + (t_out - tail0);
   }
   ts.tail = (uint32_t)t_out;
+  ts.fresh = 0u;  // every car is in the slot rows now
   return 0;
 }
 
