@@ -173,9 +173,6 @@ def main():
     ap.add_argument("--envs", type=int, default=0, help="override the batch (envs over all GPUs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--timing-every", type=int, default=0,
-                    help="launches of the event-bracketed kernel pass after the timed window (kernel duration "
-                         "for the roofline); default max(16, min(64, steps))")
     ap.add_argument("--dist", action="store_true",
                     help="initialise the process group and run the counter all-reduce on the device even "
                          "at world size 1 (RCCL check on a one-GPU box; use under torch.distributed.run)")
@@ -256,17 +253,11 @@ def main():
     window_ms = ev0.elapsed_time(ev1)
     steps1, eps1 = env.counters()
     maps1 = env.queue_maps()
-    # the step kernel's own launch duration for the roofline, after the timed window: every launch of
-    # a second pass bracketed with a HIP event pair (the same kernels on the same stream, continuing
-    # the rollout; not part of `value`)
-    kpass = args.timing_every or max(16, min(64, args.steps))
-    env.enable_timing(1)
-    env.timing_read(reset=True)
-    for k in range(kpass):  # (every rank: the ranks' trajectories stay those of a one-GPU run)
-        env.step_random(act_seed ^ 0xA5A5, k, env_offset=shard.offset)
-    torch.cuda.synchronize(dev)
-    kern_ms, launches = env.timing_read(reset=True)
-    env.enable_timing(0)
+    # the step kernel's average launch duration for the roofline: the event pair around the timed
+    # window divided by the launches (back-to-back launches on one stream: the window is their device
+    # time; it agrees with rocprofv3's per-kernel average to < 0.5 %, profiles/r04/f2, while brackets
+    # around single launches add their own gaps: +24 % on the 22-us configs[1] kernel)
+    kern_ms, launches = window_ms, args.steps
     # RCCL (nccl backend) all-reduce: global env-step / episode counters (sum), slowest rank's time (max)
     total_steps, total_eps, t_max = reduce_counters(steps1 - steps0, eps1 - eps0, elapsed, device=red_dev,
                                                     force=args.dist)
@@ -319,8 +310,7 @@ def main():
                          "peak_spec": PEAK_HBM_SPEC_GBS, "frac_spec": achieved / PEAK_HBM_SPEC_GBS,
                          "kernel": env.step_kernel() + " (step + in-kernel auto-reset)",
                          "avg_kernel_us": avg_kernel_s * 1e6, "timed_launches": launches,
-                         "kernel_timing": "HIP event pair per launch, separate pass after the timed window",
-                         "window_gpu_us_per_step": 1e3 * window_ms / args.steps,
+                         "kernel_timing": "HIP event pair around the timed window on the launch stream / launches",
                          "alg_bytes_per_launch": alg, "alg_model": "SURVEY.md 8(d)",
                          "resets_per_launch": resets_per_launch, "cars_per_env": cars,
                          "envs_per_workgroup": env.launch_info()[0], "lds_bytes": env.launch_info()[1],

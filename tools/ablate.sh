@@ -7,6 +7,6 @@ export PGTG_LIB=$PWD/pgtg_amd/libpgtg_hip_tuning.so
 for rep in 1 2; do
   for a in 0 1 2 4 6 7; do
     PGTG_ABL=$a timeout -k 10 120 python bench.py --workload $W --steps 200 --warmup 20 --no-cpu-baseline > $O/abl_$a.json 2> $O/abl_$a.err || { tail -5 $O/abl_$a.err; exit 1; }
-    python -c "import json; d=json.load(open('$O/abl_$a.json')); r=d['roofline']; print('abl=$a rep $rep', f\"kern {r['avg_kernel_us']:.1f}us window {r['window_gpu_us_per_step']:.1f}us\")"
+    python -c "import json; d=json.load(open('$O/abl_$a.json')); r=d['roofline']; print('abl=$a rep $rep', f\"kern {r['avg_kernel_us']:.1f}us\")"
   done
 done

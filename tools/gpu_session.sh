@@ -68,7 +68,7 @@ for S in "$@"; do
         python tools/bench_line.py $O/shard_$N.json
       done ;;
     profile:*)
-      timeout -k 10 1500 bash tools/gpu_profile.sh $TAG ${S#profile:} > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
+      R=${S#profile:}; timeout -k 10 1500 bash tools/gpu_profile.sh $TAG ${R//,/ } > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
       tail -5 $O/profile.log ;;
     genbench)
       timeout -k 10 120 python tools/genbench.py 5 1024 8 > $O/genbench.log 2>&1 || { tail -20 $O/genbench.log; exit 1; }
