@@ -2360,6 +2360,7 @@ struct Lds {
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
 constexpr uint64_t kStaggerMaxTicks = 20000;  // 200 us of 100 MHz wall clock: a bound, never reached
 constexpr int kQueueDepth = 3;   // queued maps per env (a ring)
+constexpr int kViewDw = 8;       // k_envq with <= 32 envs: an env's view words for the image builders
 
 __host__ __device__ inline int odd_up(int x) { return x | 1; }
 // words of a dense observation image of `envs` envs (+2: the writers' funnel reads run one word
@@ -2401,7 +2402,9 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
 // After the observation image: sel[kBlock] | 32 B (k_env: per-wave reset ballots) or 128 B (k_envq:
 // refill masks, barrier counter) | the terminal-observation line mask (lm_words) | k_envq: the
 // refill lanes' plan scratch (gen_off).  Recomputed whenever the image size changes.
-__host__ inline int tail_bytes(const Lds& l) { return kBlock + (l.queue ? 128 : 32) + 4 * l.lm_words; }
+__host__ inline int tail_bytes(const Lds& l) {
+  return kBlock + (l.queue ? 128 : 32) + 4 * l.lm_words + (l.queue && l.envs <= 32 ? 4 * kViewDw * l.envs : 0);
+}
 __host__ inline void lds_tail(Lds& l, const DevCfg& c) {
   // line mask: one bit per 128-byte output line of a whole-workgroup image (<= 64 words), else the
   // writers test the per-env selection bytes
@@ -2874,34 +2877,49 @@ __device__ __forceinline__ void sub_barrier(uint32_t* ctr, uint32_t target) {
 // observations, synchronising among themselves only.  Only when some env's ring is empty (the
 // first step after a reset, or a refill carried over) do they wait for the head refills.
 // The map-queue step's observation images.  With <= 32 envs per workgroup they all sit in wave 0
-// and most of its lanes are idle, so each env's image is built by a group of G = 64 / E lanes (up to
-// 4): lane e (the env's own) and lanes e + E, e + 2E, ... take a quarter of the channels each (their
-// bit sinks merge at the shared words), the env's lane also the next-subgoal direction.  `want`:
-// this lane's env needs an image.  Otherwise every env lane builds its own.
+// and most of its lanes are idle, so each env's image is built by a group of G = 192 / E lanes of
+// the three non-helper waves (the env wave publishes its envs' views in LDS): lane e of wave 0 (the
+// env's own) and the lanes of rank e + E, e + 2E, ... take 1/G of the channels each (their bit sinks
+// merge at the shared words), the env's lane also the next-subgoal direction.  `want`: this lane's
+// env needs an image.  Otherwise every env lane builds its own.  Called by every non-helper wave;
+// with <= 32 envs it synchronises them once (the running sub_barrier target `bar`).
 template <bool BIG>
 __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, const EnvView& v, bool want,
-                                          uint32_t* st, ObsInfo& oi, const Lds& L, int wave, int lane, bool post = true) {
+                                          uint32_t* st, ObsInfo& oi, const Lds& L, int wave, int lane,
+                                          uint32_t* ctr, uint32_t& bar, int np, int rank, uint32_t* vw,
+                                          bool post = true) {
   const int vtid = wave * 64 + lane;
   const int E = L.envs;
   if (E <= 32) {
-    if (wave != 0) return;
+    if (wave == 0 && lane < E) {
+      uint32_t* q = vw + lane * kViewDw;
+      q[0] = (uint32_t)v.px;
+      q[1] = (uint32_t)v.py;
+      q[2] = v.sg;
+      q[3] = v.phase;
+      q[4] = (uint32_t)v.used;
+      q[5] = (uint32_t)(v.used >> 32);
+      q[6] = want ? 1u : 0u;
+    }
+    sub_barrier(ctr, bar += (uint32_t)np);
     STAMP(post ? 9 : 16);
-    const int G = 64 / E, e = lane & (E - 1), sub = lane / E;
+    const int G = np * 64 / E, e = rank % E, sub = rank / E;
+    if (sub >= G) return;
+    const uint32_t* q = vw + e * kViewDw;
+    if (!q[6]) return;
+    const int C = c.n_channels, lo = sub * C / G, hi = (sub + 1) * C / G;
+    if (lo == hi && sub != 0) return;
     EnvView ve{};
-    ve.px = __shfl(v.px, e);
-    ve.py = __shfl(v.py, e);
-    ve.sg = (uint32_t)__shfl((int)v.sg, e);
-    ve.phase = (uint32_t)__shfl((int)v.phase, e);
-    ve.used = (uint64_t)(uint32_t)__shfl((int)(uint32_t)v.used, e) |
-              (uint64_t)(uint32_t)__shfl((int)(uint32_t)(v.used >> 32), e) << 32;
-    const int w_e = __shfl(want ? 1 : 0, e);
-    if (!w_e) return;
+    ve.px = (int)q[0];
+    ve.py = (int)q[1];
+    ve.sg = q[2];
+    ve.phase = q[3];
+    ve.used = (uint64_t)q[4] | (uint64_t)q[5] << 32;
     STAMP(post ? 10 : 17);
-    const int C = c.n_channels;
     extern __shared__ uint32_t lds[];
     const Plan pl{reinterpret_cast<uint16_t*>(lds + e * L.plan_stride_dw)};
-    build_obs<false, BIG, false>(c, S, pl, ve, st, (uint32_t)e * (uint32_t)c.obs_bytes, oi, nullptr, sub * C / G,
-                     (sub + 1) * C / G, sub == 0, true);
+    build_obs<false, BIG, false>(c, S, pl, ve, st, (uint32_t)e * (uint32_t)c.obs_bytes, oi, nullptr, lo, hi, sub == 0,
+                                 true);
     STAMP(post ? 11 : 18);
     return;
   }
@@ -2938,6 +2956,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   uint64_t* fm = reinterpret_cast<uint64_t*>(sel + kBlock);  // [level][env wave]: envs refilled at ring level
   uint32_t* ctr = reinterpret_cast<uint32_t*>(fm + 3 * kQueueDepth);  // sub_barrier counter
   uint32_t* lm = L.lm_words ? reinterpret_cast<uint32_t*>(sel + kBlock + 128) : nullptr;  // terminal lines
+  uint32_t* vw = reinterpret_cast<uint32_t*>(sel + kBlock + 128) + L.lm_words;  // env views (<= 32 envs)
   Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
 
   EnvView v{};
@@ -3020,6 +3039,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   // ---- env and writer waves (all but the refill wave) ----
   const int np = kBlock / 64 - 1;                            // participating waves
   const int rank = (wave < gen_wave ? wave : wave - 1) * 64 + lane, nthr = np * 64;
+  uint32_t bar = 0;  // running sub_barrier target
   uint8_t my_sel = 0;
   int err = 0;
   if (live) {
@@ -3042,7 +3062,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   // the post-step image of every env (terminal for the finished ones)
   {
     ObsInfo oi;
-    group_obs<BIG>(c, S, v, live, st, oi, L, wave, lane);
+    group_obs<BIG>(c, S, v, live, st, oi, L, wave, lane, ctr, bar, np, rank, vw);
     if (live) write_small_outputs(c, out, i, v, oi, my_sel == 1);
   }
   if (env_wave) sel[slot] = my_sel;
@@ -3050,12 +3070,12 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   if (env_wave && lane == 0 && rm) atomicAdd(&S.counters[1], (unsigned long long)__popcll(rm));
   STAMP(2);
   STAMP(28);
-  sub_barrier(ctr, (uint32_t)np);
+  sub_barrier(ctr, bar += (uint32_t)np);
   STAMP(29);
   if (out.final_obs && !(L.abl & 2))
     write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, rank, nthr, lm);
   STAMP(3);
-  sub_barrier(ctr, 2u * np);  // terminal images written before they are rebuilt
+  sub_barrier(ctr, bar += (uint32_t)np);  // terminal images written before they are rebuilt
   if (any_empty) __syncthreads();  // the head refills
   const bool reset_now = my_sel != 0;
   if (reset_now) {  // the ring's head becomes the episode (env_reset without the generation)
@@ -3128,11 +3148,11 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   STAMP(5);
   {
     ObsInfo oi;
-    group_obs<BIG>(c, S, v, reset_now, st, oi, L, wave, lane, false);
+    group_obs<BIG>(c, S, v, reset_now, st, oi, L, wave, lane, ctr, bar, np, rank, vw, false);
     if (reset_now) write_small_outputs(c, out, i, v, oi, false);
   }
   STAMP(30);
-  sub_barrier(ctr, 3u * np);
+  sub_barrier(ctr, bar += (uint32_t)np);
   STAMP(31);
   if (out.obs && !(L.abl & 4))
     write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr, rank, nthr);
