@@ -66,6 +66,7 @@ struct DevCfg {
   int32_t n_channels, win, sliding, ss, next_subgoal, generic_channels;
   int32_t channels[PGTG_MAX_CHANNELS];
   int32_t need_car, need_ice, need_broken, need_sand;
+  uint32_t zero_ch;  // channel codes (< 32) that are all-zero under this config (observation fast path)
   double density;
   uint64_t profile_t[5];  // profile CDF as 53-bit thresholds: random() < cdf[j]  <=>  (next64 >> 11) < t[j]
   int32_t car_cap;      // cars an env can hold (initial traffic <= this; pgtg_add_car / set_to_state limit)

@@ -1534,6 +1534,18 @@ struct BitSink {
       w++;
     }
   }
+  // append n zero bits (a run of all-zero channels): whole words become plain zero stores
+  __device__ __forceinline__ void skip(uint32_t n) {
+    fill += n;
+    if (fill >= 32u) {
+      emit((uint32_t)acc, own);
+      own = ~0u;
+      acc = 0;
+      fill -= 32u;
+      w++;
+      for (; fill >= 32u; fill -= 32u) st[w++] = 0u;
+    }
+  }
   __device__ __forceinline__ void finish() {
     if (fill) emit((uint32_t)acc, own & ((1u << fill) - 1u));
   }
@@ -1543,7 +1555,8 @@ struct BitSink {
 // the window's squares row-major over x, then y.
 // Channels [ch_lo, ch_hi) only (default all) when the lanes of a group share one env's image (the
 // group's sinks merge at their shared words); `head`: also the next-subgoal direction.
-template <bool TR, bool BIG, bool LC = true>  // LC: lane / spawner channels possible (they read sTX)
+template <bool TR, bool BIG, bool LC = true, bool ZS = true>  // LC: lane / spawner channels possible (they read sTX);
+                                                               // ZS: all-zero channels appended as zero runs
 __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, const Plan& pl, const EnvView& v,
                                           uint32_t* img, uint32_t bit0, ObsInfo& oi, const uint8_t* occ,
                                           int ch_lo = 0, int ch_hi = -1, bool head = true, bool lane_codes = false,
@@ -1617,8 +1630,17 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
       OB[k] = ot ? (obk & ~W3[k]) : 0u;
     }
     STAMP(19);
+    uint32_t gap = 0;  // bits of all-zero channels not yet appended
     for (int ci = ch_lo; ci < ch_hi; ci++) {
       const int code = lane_codes ? (int)sT.chan[ci] : c.channels[ci];
+      if (ZS && code < 32 && ((c.zero_ch >> code) & 1u)) {
+        gap += 81u;
+        continue;
+      }
+      if (gap) {
+        sink.skip(gap);
+        gap = 0;
+      }
       uint32_t out3[3];
 #pragma unroll
       for (int k = 0; k < 3; k++) {
@@ -1645,6 +1667,7 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
       sink.put(out3[1], 32u);
       sink.put(out3[2] & 0x1ffffu, 17u);  // 81 = 32 + 32 + 17 bits
     }
+    if (gap) sink.skip(gap);
   } else {
     const int win = c.win;
     for (int ci = ch_lo; ci < ch_hi; ci++) {
@@ -2463,7 +2486,7 @@ __device__ __forceinline__ void obs_pass(const DevCfg& c, const DevState& S, con
     const int cnt = min(L.sub_envs, nb - sb);
     if (want && slot >= sb && slot < sb + cnt) {
       ObsInfo oi;
-      build_obs<TR, BIG>(c, S, pl, v, st, (uint32_t)(slot - sb) * (uint32_t)c.obs_bytes, oi, occ);
+      build_obs<TR, BIG, true, !TR>(c, S, pl, v, st, (uint32_t)(slot - sb) * (uint32_t)c.obs_bytes, oi, occ);
       write_small_outputs(c, o, env0 + slot, v, oi, final);
     }
     lds_barrier();
@@ -2701,7 +2724,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
   if (single) {
     if (live && (my_sel != 2)) {
       ObsInfo oi;
-      build_obs<TR, BIG>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, occ_img, 0, -1, true, false, img_traf);
+      build_obs<TR, BIG, true, !TR>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, occ_img, 0, -1, true, false, img_traf);
       write_small_outputs(c, out, i, v, oi, my_sel == 1);
     }
     if (L.compact && reset_now) xf[0] = v.spawn;  // after the terminal image read the counters
@@ -2790,7 +2813,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
     if (helpers && !L.compact) lds_barrier();  // the terminal observations are written before slots are rebuilt
     if (reset_now) {
       ObsInfo oi;
-      build_obs<TR, BIG>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);  // cars come from k_traffic
+      build_obs<TR, BIG, true, !TR>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);  // cars come from k_traffic
       write_small_outputs(c, out, i, v, oi, false);
     }
     STAMP(30);
@@ -2918,7 +2941,7 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
     STAMP(post ? 10 : 17);
     extern __shared__ uint32_t lds[];
     const Plan pl{reinterpret_cast<uint16_t*>(lds + e * L.plan_stride_dw)};
-    build_obs<false, BIG, false>(c, S, pl, ve, st, (uint32_t)e * (uint32_t)c.obs_bytes, oi, nullptr, lo, hi, sub == 0,
+    build_obs<false, BIG, false, false>(c, S, pl, ve, st, (uint32_t)e * (uint32_t)c.obs_bytes, oi, nullptr, lo, hi, sub == 0,
                                  true);
     STAMP(post ? 11 : 18);
     return;
@@ -2927,7 +2950,7 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
     extern __shared__ uint32_t lds[];
     const int slot = vtid;
     const Plan pl{reinterpret_cast<uint16_t*>(lds + slot * L.plan_stride_dw)};
-    build_obs<false, BIG, false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
+    build_obs<false, BIG, false, false>(c, S, pl, v, st, (uint32_t)slot * (uint32_t)c.obs_bytes, oi, nullptr);
   }
 }
 
@@ -3698,9 +3721,16 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
   c.need_ice = kinds[0];
   c.need_broken = kinds[1];
   c.need_sand = kinds[2];
+  // observation channels no square can set: no obstacle of the kind can exist, no car
+  c.zero_ch = 1u << PGTG_CH_ZERO;
+  if (!kinds[0]) c.zero_ch |= 1u << PGTG_CH_ICE;
+  if (!kinds[1]) c.zero_ch |= 1u << PGTG_CH_BROKEN;
+  if (!kinds[2]) c.zero_ch |= 1u << PGTG_CH_SAND;
+  if (!kinds[3]) c.zero_ch |= 1u << PGTG_CH_TL_GREEN | 1u << PGTG_CH_TL_YELLOW | 1u << PGTG_CH_TL_RED;
   c.density = in.traffic_density;
   c.manual_cars = in.min_car_capacity > 0;
   c.need_car = in.traffic_density > 0 || c.manual_cars;
+  if (!c.need_car) c.zero_ch |= 1u << PGTG_CH_TRAFFIC;
   if (c.need_car) {
     if (c.W > 255 || c.H > 255) return fail(h, PGTG_E_UNSUPPORTED, "traffic needs maps of at most 28x28 tiles");
     int cap = (int)((double)(c.nt * 32) * in.traffic_density);
