@@ -41,6 +41,19 @@ WORKLOADS = {
              1048576, dict(random_map_width=5, random_map_height=5)),
     "cfg3": (2, "65536 envs, 5x5 procedural map, traffic density 0.5, random actions, auto-reset",
              65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5)),
+    # not a BASELINE config: the reference's own caller (pgtg/train.py:21-40, PGTGEnv kwargs + TimeLimit(100))
+    # at a GPU-sized batch -- the generic observation path (sliding window, next-subgoal direction),
+    # obstacles and traffic together
+    "train": (None, "65536 envs with pgtg/train.py's PGTGEnv settings: 4x4 maps, obstacles 0.2, connections 0.8, "
+                    "traffic 0.2, driver mix 15/50/20/10/5, sliding window 5, next-subgoal direction, TimeLimit(100)",
+              65536, dict(random_map_width=4, random_map_height=4, random_map_obstacle_probability=0.2,
+                          random_map_percentage_of_connections=0.8, traffic_density=0.2,
+                          conservative_driver_percentage=0.15, normal_driver_percentage=0.50,
+                          aggressive_driver_percentage=0.20, elderly_driver_percentage=0.10,
+                          reckless_driver_percentage=0.05, sliding_observation_window_size=5,
+                          max_allowed_deviation=15, use_sliding_observation_window=True,
+                          use_next_subgoal_direction=True, final_goal_bonus=200, standing_still_penalty=1,
+                          max_episode_steps=100)),
 }
 
 
@@ -215,12 +228,14 @@ def main():
     if n_total % world:
         raise SystemExit(f"{n_total} envs do not split evenly over {world} ranks")
     n_local = n_total // world
+    kwargs = dict(kwargs)
+    max_steps = kwargs.pop("max_episode_steps", None)
     spec = make_spec(**kwargs)
     shard = Shard(rank, world, n_local)
     peak_copy = measure_hbm(local) if rank == 0 else 0.0
     tune = {k: v for k, v in (("envs_per_block", args.envs_per_block), ("kt_wpc", args.kt_wpc),
                               ("kt_cap", args.kt_cap)) if v} or None
-    env = PGTGVecEnv(n_local, spec=spec, device=local, autoreset=True, tune=tune)
+    env = PGTGVecEnv(n_local, spec=spec, device=local, autoreset=True, max_episode_steps=max_steps, tune=tune)
     env.reset(seed=shard.offset)  # global env g = rank*n_local + i gets seed g
     act_seed = 0x5EED
     # synthetic policy: uniform actions from a counter hash of (seed, global env, t), generated before
@@ -294,7 +309,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": 1e3 * t_max / args.steps, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "int32",
             "data": "synthetic (device uniform random actions of the global env index, seeds = global env index)",
-            "config": {"workload": f"configs[{cfg_idx}]: {desc}", "envs_total": n_total, "envs_per_gpu": n_local,
+            "config": {"workload": (f"configs[{cfg_idx}]: " if cfg_idx is not None else "caller: ") + desc,
+                       "envs_total": n_total, "envs_per_gpu": n_local,
                        "map": f"{spec.width}x{spec.height}", "traffic_density": spec.traffic_density,
                        "autoreset": True, "parallelism": f"dp{world} (env shards, no data-path collective)"},
             "episodes": total_eps, "collective": collective,

@@ -1668,6 +1668,57 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
       sink.put(out3[2] & 0x1ffffu, 17u);  // 81 = 32 + 32 + 17 bits
     }
     if (gap) sink.skip(gap);
+  } else if (TR && WW <= 128) {
+    // windows of <= 128 squares (sliding windows up to size 5) in the traffic kernel: each square is
+    // looked up once per group of kGC channels, not once per channel -- the group's words of the whole
+    // window are accumulated in registers, then appended channel by channel (the stream's order).
+    // (Not compiled into the kernels without traffic: its 20 accumulators would raise their register
+    // peak, set elsewhere in them.)
+    constexpr int kGC = 5;
+    const int win = c.win;
+    for (int cg = ch_lo; cg < ch_hi; cg += kGC) {
+      int code[kGC];
+      bool any_sp = false, any_ln = false, any_tr = false;
+#pragma unroll
+      for (int g = 0; g < kGC; g++) {
+        code[g] = cg + g < ch_hi ? (lane_codes ? (int)sT.chan[cg + g] : c.channels[cg + g]) : (int)PGTG_CH_ZERO;
+        any_sp = any_sp || code[g] == PGTG_CH_SPAWNER;
+        any_ln = any_ln || code[g] >= PGTG_CH_LANE0;
+        any_tr = any_tr || code[g] == PGTG_CH_TRAFFIC;
+      }
+      uint32_t acc[kGC][4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+#pragma unroll
+        for (int g = 0; g < kGC; g++) acc[g][k] = 0u;
+        const int nb = min(32, WW - 32 * k);
+        for (int b = 0; b < nb; b++) {
+          const int bb = 32 * k + b, i = bb / win, j = bb - i * win;
+          const int x = oi.x0 + i, y = oi.y0 + j;
+          uint32_t f, lanes = 0;
+          bool sp = false, car = false;
+          if (inside(c, x, y)) {
+            f = square_flags<BIG>(c, pl, v, x, y);
+            if (LC && any_sp) sp = square_spawner(c, pl, x, y);
+            if (LC && any_ln) lanes = square_lanes(c, pl, x, y);
+            if ((TR && c.need_car) && occ && any_tr) car = occ_at(c, pl, occ, x, y) > 0;
+          } else {
+            f = c.sliding ? SQ_WALL : 0u;  // get_map_cutout fill {"wall"} for sliding windows
+          }
+#pragma unroll
+          for (int g = 0; g < kGC; g++)
+            acc[g][k] |= (code[g] == PGTG_CH_TRAFFIC ? (car ? 1u : 0u) : chan_bit(code[g], f, lanes, sp, color)) << b;
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < kGC; g++) {
+        if (cg + g < ch_hi) {
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (32 * k < WW) sink.put(acc[g][k], (uint32_t)min(32, WW - 32 * k));
+        }
+      }
+    }
   } else {
     const int win = c.win;
     for (int ci = ch_lo; ci < ch_hi; ci++) {

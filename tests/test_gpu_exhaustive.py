@@ -96,6 +96,16 @@ CASES = {
     "features_all_names_3000": (3000, 10, dict(random_map_width=4, random_map_height=4, traffic_density=0.3,
                                                random_map_obstacle_probability=0.5,
                                                features_to_include_in_observation=ALL_FEATURES), None),
+    # the reference's training caller (pgtg/train.py:21-37; bench.py --workload train): obstacles,
+    # traffic with its driver mix, sliding window 5 and the next-subgoal direction together
+    "train_caller_8192x30": (8192, 30, dict(random_map_width=4, random_map_height=4, random_map_obstacle_probability=0.2,
+                                            random_map_percentage_of_connections=0.8, traffic_density=0.2,
+                                            conservative_driver_percentage=0.15, normal_driver_percentage=0.50,
+                                            aggressive_driver_percentage=0.20, elderly_driver_percentage=0.10,
+                                            reckless_driver_percentage=0.05, sliding_observation_window_size=5,
+                                            max_allowed_deviation=15, use_sliding_observation_window=True,
+                                            use_next_subgoal_direction=True, final_goal_bonus=200,
+                                            standing_still_penalty=1), None),
     "cfg2_wg256_sub32": (4096, 40, dict(random_map_width=3, random_map_height=3),
                          dict(envs_per_block=256, obs_sub=32)),
     "cfg5_wg256": (65536, 20, dict(random_map_width=5, random_map_height=5), dict(envs_per_block=256)),
