@@ -3307,7 +3307,8 @@ __global__ void __launch_bounds__(kBlock) k_gen_bench(const DevCfg* __restrict__
 #endif
 
 // Initial traffic of the envs k_env reset in this launch (its work list) with the reset scratch in
-// LDS; the observation k_env wrote for them gets the new cars' squares.  One workgroup per CU, and
+// LDS; the observation k_env wrote for them gets the new cars' squares (traffic channel only: the
+// agent's tile window from the group's CR, other windows from the square list).  One workgroup per CU, and
 // the list is spread evenly over all of their waves: a wave's time is its envs' serial chain whatever
 // the number of active lanes, so the envs per wave are levelled first (`e`, at most `cap_w` in LDS
 // at once, in rounds beyond that), then the wave's 64 lanes are shared out: 4 per env up to 16
@@ -3358,7 +3359,24 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
     const int err = traffic_reset(c, S, i, pl, cr, rs, ts, at, CR, sub, g);
     const int q0 = lane - sub;  // (traffic_reset's result is lane 0's)
     const int err0 = __shfl(err, q0), k0 = __shfl((int)ts.n_cars, q0);
-    if (err0 == 0) store_initial_counters(c, S, i, pl, rs, k0, sub, g);
+    if (err0 == 0) {
+      store_initial_counters(c, S, i, pl, rs, k0, sub, g);
+      if (!c.obs_fast && c.traffic_ch >= 0 && out.obs && k0 > 0) {
+        // generic windows (sliding, lane channels): k_env built this observation without cars; the
+        // traffic channel -- the only one cars change -- gets the new cars' squares inside the window
+        // (the group's lanes take every g-th car of the square list traffic_reset left in rs)
+        const int win = c.win;
+        const int x0 = c.sliding ? v.px - c.ss : (pix / kTile) * kTile;
+        const int y0 = c.sliding ? v.py - c.ss : (piy / kTile) * kTile;
+        const uint16_t* sqs = reinterpret_cast<const uint16_t*>(rs);
+        uint8_t* o = out.obs + i * (uint64_t)c.obs_bytes + (uint64_t)c.traffic_ch * (uint64_t)(win * win);
+        for (int m = sub; m < k0; m += g) {
+          const uint32_t code = sqs[m];
+          const int a = (int)(code & 255u) - x0, b = (int)(code >> 8) - y0;
+          if (a >= 0 && a < win && b >= 0 && b < win) o[a * win + b] = 1;
+        }
+      }
+    }
     if (sub == 0) {
       stream_store_state(S.car, i, cr);
       S.traf[i] = make_uint4(ts.n_cars | ts.n_spawners << 16, ts.next_id, ts.tail, err == 0 ? kTrafOccValid | kTrafFresh : 0u);
@@ -4196,22 +4214,11 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
   }
   HIPCHK(h, hipGetLastError());
   if (h->hcfg.need_car && mode != MODE_OBSERVE) {
-    // initial traffic of the envs reset by this launch, then (windows other than the agent's tile)
-    // their observation again with the cars
+    // initial traffic of the envs reset by this launch; it also sets their new cars' squares in the
+    // observation's traffic channel
     hipLaunchKernelGGL(k_traffic, dim3((unsigned)h->kt_grid), dim3(kBlock), h->kt_lds, h->stream, h->dcfg, h->dtab,
                        h->S, h->out, h->tr_slot, h->kt_plan_dw, h->kt_rs_dw, h->kt_cap);
     HIPCHK(h, hipGetLastError());
-    if (!h->hcfg.obs_fast && h->hcfg.traffic_ch >= 0) {
-      PgtgOutputs o{};
-      o.obs = h->out.obs;  // only the observation: positions etc. are unchanged
-      if (h->hcfg.nt > kSmallTiles)
-        hipLaunchKernelGGL((k_env<true, true>), dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab,
-                           h->S, nullptr, nullptr, o, (int)MODE_OBSERVE, h->L, h->tr_slot);
-      else
-        hipLaunchKernelGGL((k_env<true, false>), dim3((unsigned)blocks), dim3(kBlock), h->lds, h->stream, h->dcfg, h->dtab,
-                           h->S, nullptr, nullptr, o, (int)MODE_OBSERVE, h->L, h->tr_slot);
-      HIPCHK(h, hipGetLastError());
-    }
     h->tr_slot ^= 1u;
   }
   if (timed) {
