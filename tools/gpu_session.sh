@@ -75,7 +75,7 @@ for S in "$@"; do
       tail -1 $O/genbench.log ;;
     stamps:*)
       python -c "from pgtg_amd.build import build; build(variant='stamps')" || exit 1
-      timeout -k 10 300 python tools/stamps.py ${S#stamps:} > $O/stamps.log 2>&1 || { tail -20 $O/stamps.log; exit 1; }
+      R=${S#stamps:}; timeout -k 10 300 python tools/stamps.py ${R//,/ } > $O/stamps.log 2>&1 || { tail -20 $O/stamps.log; exit 1; }
       cat $O/stamps.log ;;
     stampsjson:*)
       W=${S#stampsjson:}

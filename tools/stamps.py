@@ -35,6 +35,8 @@ CASES = {"cfg2": (4096, dict(random_map_width=3, random_map_height=3)),
          "cfg5big": (1048576, dict(random_map_width=5, random_map_height=5)),
          "cfg4": (262144, dict(random_map_width=3, random_map_height=3)),
          "cfg3": (65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5))}
+import bench  # noqa: E402  (the caller workload: pgtg/train.py's settings)
+CASES["train"] = (bench.WORKLOADS["train"][2], dict(bench.WORKLOADS["train"][3]))
 for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
     N, kw = CASES[name]
     env = PGTGVecEnv(N, device=0, **kw)
