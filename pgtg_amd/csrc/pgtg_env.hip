@@ -1692,7 +1692,8 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
 #pragma unroll
         for (int g = 0; g < kGC; g++) acc[g][k] = 0u;
         const int nb = min(32, WW - 32 * k);
-        for (int b = 0; b < nb; b++) {
+#pragma unroll 4
+        for (int b = 0; b < nb; b++) {  // (unrolled: four squares' LDS lookups go out together)
           const int bb = 32 * k + b, i = bb / win, j = bb - i * win;
           const int x = oi.x0 + i, y = oi.y0 + j;
           uint32_t f, lanes = 0;
