@@ -1677,14 +1677,33 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
     constexpr int kGC = 5;
     const int win = c.win;
     for (int cg = ch_lo; cg < ch_hi; cg += kGC) {
-      int code[kGC];
+      // each channel of the group as a branch-free test of the square's words (chan_bit's cases):
+      // a flag mask, or the spawner / traffic bit, or a lane bit
+      uint32_t fm[kGC];
+      int lb[kGC];
+      bool is_sp[kGC], is_tr[kGC];
       bool any_sp = false, any_ln = false, any_tr = false;
 #pragma unroll
       for (int g = 0; g < kGC; g++) {
-        code[g] = cg + g < ch_hi ? (lane_codes ? (int)sT.chan[cg + g] : c.channels[cg + g]) : (int)PGTG_CH_ZERO;
-        any_sp = any_sp || code[g] == PGTG_CH_SPAWNER;
-        any_ln = any_ln || code[g] >= PGTG_CH_LANE0;
-        any_tr = any_tr || code[g] == PGTG_CH_TRAFFIC;
+        const int code = cg + g < ch_hi ? (lane_codes ? (int)sT.chan[cg + g] : c.channels[cg + g]) : (int)PGTG_CH_ZERO;
+        fm[g] = code == PGTG_CH_WALL ? SQ_WALL
+              : code == PGTG_CH_GOALS ? (SQ_SUBGOAL | SQ_FINAL)
+              : code == PGTG_CH_TL_GREEN ? (color == 0 ? SQ_TLIGHT : 0u)
+              : code == PGTG_CH_TL_YELLOW ? (color == 1 ? SQ_TLIGHT : 0u)
+              : code == PGTG_CH_TL_RED ? (color == 2 ? SQ_TLIGHT : 0u)
+              : code == PGTG_CH_START ? SQ_START
+              : code == PGTG_CH_SUBGOAL ? SQ_SUBGOAL
+              : code == PGTG_CH_USED_SUBGOAL ? SQ_USED
+              : code == PGTG_CH_FINAL_GOAL ? SQ_FINAL
+              : code == PGTG_CH_ICE ? SQ_ICE
+              : code == PGTG_CH_BROKEN ? SQ_BROKEN
+              : code == PGTG_CH_SAND ? SQ_SAND : 0u;
+        is_sp[g] = code == PGTG_CH_SPAWNER;
+        is_tr[g] = code == PGTG_CH_TRAFFIC;
+        lb[g] = (code >= PGTG_CH_LANE0 && code < PGTG_CH_LANE0 + 32) ? code - PGTG_CH_LANE0 : -1;
+        any_sp = any_sp || is_sp[g];
+        any_ln = any_ln || lb[g] >= 0;
+        any_tr = any_tr || is_tr[g];
       }
       uint32_t acc[kGC][4];
 #pragma unroll
@@ -1696,19 +1715,24 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
         for (int b = 0; b < nb; b++) {  // (unrolled: four squares' LDS lookups go out together)
           const int bb = 32 * k + b, i = bb / win, j = bb - i * win;
           const int x = oi.x0 + i, y = oi.y0 + j;
-          uint32_t f, lanes = 0;
+          // every lookup at clamped coordinates, then selected: no divergent branch per square
+          const bool in = inside(c, x, y);
+          const int xc = min(max(x, 0), c.W - 1), yc = min(max(y, 0), c.H - 1);
+          uint32_t f = square_flags<BIG>(c, pl, v, xc, yc), lanes = 0;
           bool sp = false, car = false;
-          if (inside(c, x, y)) {
-            f = square_flags<BIG>(c, pl, v, x, y);
-            if (LC && any_sp) sp = square_spawner(c, pl, x, y);
-            if (LC && any_ln) lanes = square_lanes(c, pl, x, y);
-            if ((TR && c.need_car) && occ && any_tr) car = occ_at(c, pl, occ, x, y) > 0;
-          } else {
-            f = c.sliding ? SQ_WALL : 0u;  // get_map_cutout fill {"wall"} for sliding windows
-          }
+          if (LC && any_sp) sp = square_spawner(c, pl, xc, yc);
+          if (LC && any_ln) lanes = square_lanes(c, pl, xc, yc);
+          if ((TR && c.need_car) && occ && any_tr) car = occ_at(c, pl, occ, xc, yc) > 0;
+          f = in ? f : (c.sliding ? SQ_WALL : 0u);  // get_map_cutout fill {"wall"} for sliding windows
+          lanes = in ? lanes : 0u;
+          sp = in && sp;
+          car = in && car;
 #pragma unroll
-          for (int g = 0; g < kGC; g++)
-            acc[g][k] |= (code[g] == PGTG_CH_TRAFFIC ? (car ? 1u : 0u) : chan_bit(code[g], f, lanes, sp, color)) << b;
+          for (int g = 0; g < kGC; g++) {
+            const uint32_t bit = ((f & fm[g]) != 0u ? 1u : 0u) | (is_sp[g] && sp ? 1u : 0u) | (is_tr[g] && car ? 1u : 0u) |
+                                 (lb[g] >= 0 ? (lanes >> (lb[g] & 31)) & 1u : 0u);
+            acc[g][k] |= bit << b;
+          }
         }
       }
 #pragma unroll
