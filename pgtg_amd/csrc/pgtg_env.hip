@@ -3980,10 +3980,12 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
     // k_traffic: per-lane plan + reset scratch
     h->kt_plan_dw = odd_up((c.nt + 1) / 2);
     h->kt_rs_dw = odd_up(c.rs_bytes / 4);
-    // workgroups per CU (one: a second wave per SIMD measured slower than more envs per wave),
-    // then the envs per wave that fit the LDS of that many workgroups
+    // workgroups per CU (two: a second wave per SIMD hides part of the per-lane LDS latency --
+    // round 4, configs[2] 910 -> 877 us and the caller workload 733 -> 695 us per step against one,
+    // profiles/r04/x17; an earlier tree had measured one faster), then the envs per wave that fit the
+    // LDS of that many workgroups
     const size_t per_env = (size_t)4 * (h->kt_plan_dw + h->kt_rs_dw);
-    int wpc = h->tune_kt_wpc ? std::max(1, std::min(4, h->tune_kt_wpc)) : 1;
+    int wpc = h->tune_kt_wpc ? std::max(1, std::min(4, h->tune_kt_wpc)) : 2;
     for (;; wpc--) {
       h->kt_cap = 32;  // envs per wave held in LDS at once
       while (h->kt_cap > 1 && wpc * (4 * h->kt_cap * per_env + sizeof(Tables) + 256) > 160 * 1024) h->kt_cap--;
