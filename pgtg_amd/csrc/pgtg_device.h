@@ -54,6 +54,7 @@ struct DevCfg {
   uint32_t fixed_sg;
   int32_t start_mode, goal_mode, sx, sy, sdir, gx, gy, gdir, min_distance;
   int32_t n_edges, keep;
+  int32_t dual;       // the edge-removal test runs on the dual (wall) graph: >= 2 x 2, <= 64 tiles, w + h <= 31
   uint64_t h0[4][4];  // full-grid exit masks before removals: h0[64-tile word][N, E, S, W]
   int32_t n_border, n_border_add;
   uint8_t bt[kMaxBorder], bd[kMaxBorder];
@@ -116,6 +117,9 @@ struct TablesHead {
   // removable edges in graph-theory order, oriented: a | b<<8 | horizontal<<16 | reverse edge<<17 with
   // a the north/west tile (maps of <= 64 tiles; larger maps read DevState::epk)
   uint32_t epk[kSmallEdges];
+  // per epk entry the removed edge's wall: corner codes p | q << 8 (interior corner (cy-1)(w-1) + cx-1,
+  // or 64 + boundary position clockwise from the north-west corner), when DevCfg::dual
+  uint16_t ewl[kSmallEdges];
   uint8_t bt[kMaxBorder], bd[kMaxBorder];
   // observation channel codes (DevCfg::channels as bytes): read per lane when the lanes of a group
   // build different channels of one env's image (a per-lane index into the DevCfg block would be a

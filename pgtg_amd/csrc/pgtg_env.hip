@@ -675,6 +675,112 @@ __device__ __forceinline__ void remove_edges(const DevCfg& c, const uint32_t* __
 #endif
 }
 
+// The same loop decided on the dual graph (round 5; maps of <= 64 tiles, both sides >= 2, w + h <= 31).
+// A removed edge is a wall segment between two corners of the tile grid.  Start s and goal g are border
+// tiles, so their boundary segments split the outer boundary's corners into two arcs, A (clockwise
+// from s to g) and B (from g back to s); s and g are disconnected iff walls join a corner of A to a
+// corner of B (the planar separation of two boundary cells).  RA / RB hold the interior corners
+// wall-connected to A / B, so a removal is undone iff its wall would join RA u A to RB u B: four bit
+// tests instead of a flood of the tile graph.  A kept wall that attaches a corner to RA (RB) adds that
+// corner's wall component, found by a flood over the interior walls that is usually one expansion
+// (a fresh corner).  Checked against BFS connectivity on every border start/goal pair of 2x2 .. 8x8
+// grids; the RNG draws, the removable list and the outcomes are the primal loop's.
+struct DualArcs {
+  uint64_t ba, bb;  // boundary corner positions (clockwise from the north-west corner) on arc A, arc B
+};
+// boundary segments of border tile t: the run [r0, r0 + len) of segment indices (segment i joins
+// boundary positions i and i + 1; corner tiles own two consecutive segments)
+__device__ __forceinline__ void border_run(int t, int w, int h, int& r0, int& len) {
+  const int L = 2 * (w + h), x = t % w, y = t / w;
+  if (y == 0) {
+    r0 = x == 0 ? L - 1 : x;
+    len = (x == 0 || x == w - 1) ? 2 : 1;
+  } else if (x == w - 1) {
+    r0 = w + y;
+    len = y == h - 1 ? 2 : 1;
+  } else if (y == h - 1) {
+    r0 = w + h + (w - 1 - x);
+    len = x == 0 ? 2 : 1;
+  } else {
+    r0 = 2 * w + h + (h - 1 - y);
+    len = 1;
+  }
+}
+// `cnt` consecutive positions from `from` on the cyclic boundary of L < 64 positions
+__device__ __forceinline__ uint64_t arc_mask(int from, int cnt, int L) {
+  const uint64_t m = cnt >= 64 ? ~0ull : (1ull << cnt) - 1ull, all = (1ull << L) - 1ull;
+  return ((m << from) | (from ? m >> (L - from) : 0ull)) & all;
+}
+__device__ __forceinline__ DualArcs dual_arcs(int w, int h, int s, int g) {
+  DualArcs d{0ull, 0ull};
+  if (s == g) return d;  // one tile: never separated, no removal is undone
+  const int L = 2 * (w + h);
+  int s0, sl, g0, gl;
+  border_run(s, w, h, s0, sl);
+  border_run(g, w, h, g0, gl);
+  const int a0 = (s0 + sl) % L, b0 = (g0 + gl) % L;  // first corner after s's run, after g's run
+  d.ba = arc_mask(a0, (g0 - a0 + L) % L + 1, L);      // up to and including g's first corner
+  d.bb = arc_mask(b0, (s0 - b0 + L) % L + 1, L);
+  return d;
+}
+// corner code x (interior corner index < 64, or 64 + boundary position) in R (interior) / Bm (boundary)
+template <typename CM>
+__device__ __forceinline__ bool corner_in(int x, CM R, uint64_t Bm) {
+  const bool rb = (R >> (x & (int)(sizeof(CM) * 8 - 1))) & 1u, bb = (Bm >> (x & 63)) & 1ull;
+  return x >= 64 ? bb : rb;
+}
+template <typename M, int NW, typename CM>
+__device__ __forceinline__ void remove_edges_dual(const DevCfg& c, const uint32_t* __restrict__ epk,
+                                                  const uint16_t* __restrict__ ewl, Pcg& r, int st_t, int gl_t,
+                                                  M& hN, M& hE, M& hS, M& hW) {
+  const int w = pinned(c.tw), keep = pinned(c.keep), n_edges = pinned(c.n_edges), wi = w - 1;
+  const DualArcs da = dual_arcs(w, c.th, st_t, gl_t);
+  EdgeBits<NW> L;
+  L.init(n_edges);
+  int nrem = n_edges, count = n_edges;
+  M RH = 0, RV = 0;          // removed tile edges: RH bit a = a|a+1 (horizontal), RV bit a = a|a+w
+  CM RA = 0, RB = 0;         // interior corners wall-connected to arc A / arc B
+  CM WE = 0, WS = 0;         // interior walls: WE bit k = corner k - k+1, WS bit k = corner k - k+wi
+  while (count > keep && nrem > 0) {
+    const int k = (int)pcg_draw(r, true, (uint32_t)nrem);  // nrem >= 2: always draws
+    const int e = L.select(k);
+    const uint32_t pk = epk[e], wl = ewl[e];
+    L.clear(e);
+    L.clear((int)(pk >> 17));
+    nrem -= 2;
+    const int p = (int)(wl & 255u), q = (int)(wl >> 8);
+    const bool ap = corner_in<CM>(p, RA, da.ba), aq = corner_in<CM>(q, RA, da.ba);
+    const bool bp = corner_in<CM>(p, RB, da.bb), bq = corner_in<CM>(q, RB, da.bb);
+    if ((ap && bq) || (bp && aq)) continue;  // the wall would separate s from g: removal undone
+    count -= 2;
+    const bool hz = (pk >> 16) & 1u;
+    const M ma = (M)1 << (pk & (sizeof(M) * 8 - 1));
+    RH |= hz ? ma : (M)0;
+    RV |= hz ? (M)0 : ma;
+    if (ap != aq || bp != bq) {  // the wall attaches the other corner's component to an arc
+      const bool toA = ap != aq;
+      const int o = (toA ? ap : bp) ? q : p;  // interior (a boundary corner's side is fixed)
+      CM C = (CM)1 << (o & (int)(sizeof(CM) * 8 - 1)), N;
+      for (;;) {
+        N = C | ((C & WE) << 1) | ((C >> 1) & WE) | ((C & WS) << wi) | ((C >> wi) & WS);
+        if (N == C) break;
+        C = N;
+      }
+      RA |= toA ? C : (CM)0;
+      RB |= toA ? (CM)0 : C;
+    }
+    if ((p | q) < 64) {  // interior wall (the component floods above ran without it)
+      const CM wb = (CM)1 << (min(p, q) & (int)(sizeof(CM) * 8 - 1));
+      WS |= hz ? wb : (CM)0;
+      WE |= hz ? (CM)0 : wb;
+    }
+  }
+  hE &= ~RH;
+  hW &= ~(RH << 1);
+  hS &= ~RV;
+  hN &= ~(RV << w);
+}
+
 template <int NW>
 __device__ __forceinline__ void add_border_connections(const DevCfg& c, Pcg& r, uint16_t* plan) {
   EdgeBits<NW> B;
@@ -690,9 +796,11 @@ __device__ __forceinline__ void add_border_connections(const DevCfg& c, Pcg& r, 
 
 // generate_map (map_generator.py:43-189) -> tile plan (exits + obstacles) in LDS, start/goal
 // (BIG: maps of > 64 tiles, 256-bit masks and the global edge table `epk`)
+// `ix` (maps of <= 64 tiles, DevCfg::dual): the interior exit masks N, E, S, W of the generated graph,
+// which compile_path_m takes instead of re-reading the plan.
 template <bool BIG>
 __device__ __forceinline__ void generate_map(const DevCfg& c, const uint32_t* __restrict__ epk, Pcg& r, uint16_t* plan,
-                                             int& st_t, int& st_d, int& gl_t, int& gl_d) {
+                                             int& st_t, int& st_d, int& gl_t, int& gl_d, uint64_t* ix = nullptr) {
   const int w = c.tw;
   // chose_random_start_and_goal_position_and_direction (map_generator.py:475-571)
   int s0, s1, s2 = c.sdir, g0, g1, g2 = c.gdir;
@@ -748,25 +856,60 @@ __device__ __forceinline__ void generate_map(const DevCfg& c, const uint32_t* __
                            (uint32_t)mask_get(we, t) << 3);
   } else {
     uint64_t hN, hE, hS, hW;
-    if (c.nt <= 32) {
+    if (c.dual && c.nt <= 32) {
       uint32_t n = (uint32_t)c.h0[0][0], e = (uint32_t)c.h0[0][1], so = (uint32_t)c.h0[0][2], we = (uint32_t)c.h0[0][3];
-      if (c.n_edges <= 64) remove_edges<uint32_t, 1>(c, epk, r, st_t, gl_t, n, e, so, we);
-      else remove_edges<uint32_t, 2>(c, epk, r, st_t, gl_t, n, e, so, we);
+      if (c.n_edges <= 64) remove_edges_dual<uint32_t, 1, uint32_t>(c, epk, sT.ewl, r, st_t, gl_t, n, e, so, we);
+      else remove_edges_dual<uint32_t, 2, uint32_t>(c, epk, sT.ewl, r, st_t, gl_t, n, e, so, we);
       hN = n; hE = e; hS = so; hW = we;
     } else {
       hN = c.h0[0][0]; hE = c.h0[0][1]; hS = c.h0[0][2]; hW = c.h0[0][3];
-      remove_edges<uint64_t, 4>(c, epk, r, st_t, gl_t, hN, hE, hS, hW);
+      if (c.dual) remove_edges_dual<uint64_t, 4, uint64_t>(c, epk, sT.ewl, r, st_t, gl_t, hN, hE, hS, hW);
+      else remove_edges<uint64_t, 4>(c, epk, r, st_t, gl_t, hN, hE, hS, hW);  // 1-wide maps, w + h > 31
     }
-    for (int t = 0; t < c.nt; t++)
-      plan[t] = (uint16_t)((uint32_t)((hN >> t) & 1ull) | (uint32_t)((hE >> t) & 1ull) << 1 |
-                           (uint32_t)((hS >> t) & 1ull) << 2 | (uint32_t)((hW >> t) & 1ull) << 3);
+    if (c.dual) {
+      // The exits stay in registers: add_connections_to_borders (map_generator.py:337-371) draws
+      // candidate indices from the host's list (north row, east column from y = 1, south row, west
+      // column up to y = h - 2 -- the two entries the reference removes), so the chosen set maps to
+      // exit bits by arithmetic, and the plan is written once, two tiles per LDS word.
+      ix[0] = hN; ix[1] = hE; ix[2] = hS; ix[3] = hW;
+      const int h = c.th, nbd = pinned(c.n_border), nadd = pinned(c.n_border_add);
+      const uint64_t all = (1ull << nbd) - 1ull;
+      uint64_t B = all;
+      for (int k = 0; k < nadd; k++) B &= ~(1ull << select64(B, (int)pcg_int(r, (uint32_t)(nbd - k))));
+      const uint64_t ch = all & ~B, row = (1ull << w) - 1ull;
+      uint64_t bE = 0, bW = 0;
+      for (int y = 1; y < h; y++) {
+        bE |= ((ch >> (w + y - 1)) & 1ull) << (y * w + w - 1);
+        bW |= ((ch >> (2 * w + h - 2 + y)) & 1ull) << ((y - 1) * w);
+      }
+      const uint64_t sb = 1ull << st_t, gb = 1ull << gl_t;
+      hN |= (ch & row) | (st_d == 0 ? sb : 0ull) | (gl_d == 0 ? gb : 0ull);
+      hE |= bE | (st_d == 1 ? sb : 0ull) | (gl_d == 1 ? gb : 0ull);
+      hS |= (((ch >> (w + h - 1)) & row) << ((h - 1) * w)) | (st_d == 2 ? sb : 0ull) | (gl_d == 2 ? gb : 0ull);
+      hW |= bW | (st_d == 3 ? sb : 0ull) | (gl_d == 3 ? gb : 0ull);
+      uint32_t* pw = reinterpret_cast<uint32_t*>(plan);
+      for (int t = 0; t < c.nt; t += 2) {
+        const uint64_t x0 = hN >> t, x1 = hE >> t, x2 = hS >> t, x3 = hW >> t;
+        const uint32_t lo = (uint32_t)(x0 & 1ull) | (uint32_t)(x1 & 1ull) << 1 | (uint32_t)(x2 & 1ull) << 2 |
+                            (uint32_t)(x3 & 1ull) << 3;
+        const uint32_t hi = (uint32_t)(x0 & 2ull) >> 1 | (uint32_t)(x1 & 2ull) | (uint32_t)(x2 & 2ull) << 1 |
+                            (uint32_t)(x3 & 2ull) << 2;
+        pw[t >> 1] = lo | (t + 1 < c.nt ? hi << 16 : 0u);
+      }
+    } else {
+      for (int t = 0; t < c.nt; t++)
+        plan[t] = (uint16_t)((uint32_t)((hN >> t) & 1ull) | (uint32_t)((hE >> t) & 1ull) << 1 |
+                             (uint32_t)((hS >> t) & 1ull) << 2 | (uint32_t)((hW >> t) & 1ull) << 3);
+    }
   }
   STAMP(15);
-  plan[st_t] |= (uint16_t)(1u << st_d);
-  plan[gl_t] |= (uint16_t)(1u << gl_d);
-  // add_connections_to_borders (map_generator.py:337-371), candidate list from the host
-  if (c.n_border <= 64) add_border_connections<1>(c, r, plan);
-  else add_border_connections<3>(c, r, plan);
+  if (BIG || !c.dual) {
+    plan[st_t] |= (uint16_t)(1u << st_d);
+    plan[gl_t] |= (uint16_t)(1u << gl_d);
+    // add_connections_to_borders (map_generator.py:337-371), candidate list from the host
+    if (c.n_border <= 64) add_border_connections<1>(c, r, plan);
+    else add_border_connections<3>(c, r, plan);
+  }
   // add_obstacles_to_map (map_generator.py:374-472)
   if (c.obstacle_probability > 0.0) {
     for (int t = 0; t < c.nt; t++) {
@@ -802,9 +945,11 @@ __device__ __forceinline__ void generate_map(const DevCfg& c, const uint32_t* __
 // tiles whose N/E/S/W neighbour lies one layer closer are collected as masks, so the walk is
 // register arithmetic.  Marks the direction to the next tile on every path tile but the goal's;
 // returns the number of path tiles (0: unreachable).
+// compile_path_m: the same from the interior exit masks (generate_map's `ix`), without the plan reads.
+template <typename M>
+__device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, int s, int g, M hN, M hE, M hS, M hW);
 template <typename M>
 __device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, int s, int g) {
-  const int w = c.tw;
   M hN = mask_zero<M>(), hE = hN, hS = hN, hW = hN;
   for (int t = 0; t < c.nt; t++) {
     const uint32_t e = plan_exits(plan[t]);
@@ -818,6 +963,11 @@ __device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, int
   hE &= mask_h0<M>(c, 1);
   hS &= mask_h0<M>(c, 2);
   hW &= mask_h0<M>(c, 3);
+  return compile_path_m<M>(c, plan, s, g, hN, hE, hS, hW);
+}
+template <typename M>
+__device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, int s, int g, M hN, M hE, M hS, M hW) {
+  const int w = c.tw;
   STAMP(24);
   M vis = mask_bit<M>(g), front = vis;
   M cN = mask_zero<M>(), cE = cN, cS = cN, cW = cN;  // tiles with a neighbour one layer closer, per direction
@@ -863,6 +1013,18 @@ __device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, int
     }
   }
   return len;
+}
+
+// The path of a map generate_map<BIG> just built: from its interior exit masks `ix` when it left them
+// (small maps, DevCfg::dual), else from the plan.
+template <bool BIG>
+__device__ __forceinline__ int compile_generated(const DevCfg& c, uint16_t* plan, int s, int g, const uint64_t* ix) {
+  if (BIG) return compile_path<Bits<4>>(c, plan, s, g);
+  if (c.dual) {
+    if (c.nt <= 32) return compile_path_m<uint32_t>(c, plan, s, g, (uint32_t)ix[0], (uint32_t)ix[1], (uint32_t)ix[2], (uint32_t)ix[3]);
+    return compile_path_m<uint64_t>(c, plan, s, g, ix[0], ix[1], ix[2], ix[3]);
+  }
+  return c.nt <= 32 ? compile_path<uint32_t>(c, plan, s, g) : compile_path<uint64_t>(c, plan, s, g);
 }
 
 struct TrafState {
@@ -1387,19 +1549,23 @@ __device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uin
   v.spawn = k + 5u;
   STAMP(9);
   int st_t, st_d, gl_t, gl_d;
+  int len;
   if (c.fixed_map) {
     for (int t = 0; t < c.nt; t++) plan[t] = c.fixed_plan[t];
     st_t = (int)(c.fixed_sg & 0xffu);
     st_d = (int)((c.fixed_sg >> 8) & 0xffu);
     gl_t = (int)((c.fixed_sg >> 16) & 0xffu);
     gl_d = (int)(c.fixed_sg >> 24);
+    STAMP(10);
+    len = BIG ? compile_path<Bits<4>>(c, plan, st_t, gl_t)
+              : (c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t));
   } else {
-    generate_map<BIG>(c, BIG ? S.epk : sT.epk, map_rng, plan, st_t, st_d, gl_t, gl_d);
+    uint64_t ix[4];
+    generate_map<BIG>(c, BIG ? S.epk : sT.epk, map_rng, plan, st_t, st_d, gl_t, gl_d, ix);
+    STAMP(10);
+    len = compile_generated<BIG>(c, plan, st_t, gl_t, ix);
   }
   v.sg = (uint32_t)st_t | (uint32_t)st_d << 8 | (uint32_t)gl_t << 16 | (uint32_t)gl_d << 24;
-  STAMP(10);
-  int len = BIG ? compile_path<Bits<4>>(c, plan, st_t, gl_t)
-          : (c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t));
   STAMP(11);
   v.used = 0;
   v.path_len = (uint32_t)len;
@@ -2920,9 +3086,9 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
   SeedPool sp = ss_pool(S.seed[i]);
   Pcg map_rng = ss_child(sp, k);
   int st_t, st_d, gl_t, gl_d;
-  generate_map<BIG>(c, BIG ? S.epk : sT.epk, map_rng, plan, st_t, st_d, gl_t, gl_d);
-  const int len = BIG ? compile_path<Bits<4>>(c, plan, st_t, gl_t)
-                : (c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t));
+  uint64_t ix[4];
+  generate_map<BIG>(c, BIG ? S.epk : sT.epk, map_rng, plan, st_t, st_d, gl_t, gl_d, ix);
+  const int len = compile_generated<BIG>(c, plan, st_t, gl_t, ix);
   int px = 0, py = 0, err = 0;
   if (len == 0 || !((plan_exits(plan[st_t]) >> st_d) & 1u)) {
     err = PGTG_E_MAP;
@@ -3313,9 +3479,10 @@ __global__ void __launch_bounds__(kBlock) k_gen_bench(const DevCfg* __restrict__
       Pcg g = ss_child(sp, 5u * (uint32_t)r);
       int st_t, st_d, gl_t, gl_d;
       const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-      generate_map<false>(c, sT.epk, g, plan, st_t, st_d, gl_t, gl_d);
+      uint64_t ix[4];
+      generate_map<false>(c, sT.epk, g, plan, st_t, st_d, gl_t, gl_d, ix);
       const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-      const int len = c.nt <= 32 ? compile_path<uint32_t>(c, plan, st_t, gl_t) : compile_path<uint64_t>(c, plan, st_t, gl_t);
+      const int len = compile_generated<false>(c, plan, st_t, gl_t, ix);
       const unsigned long long t2 = __builtin_amdgcn_s_memtime();
       tg += t1 - t0;
       tc += t2 - t1;
@@ -3562,6 +3729,7 @@ struct pgtg_handle {
   uint64_t acc_n = 0;
   // k_traffic: work-list parity, grid (one workgroup per CU), envs per wave in LDS, dynamic LDS
   std::vector<uint32_t> epk;  // the map's edge table (derive_cfg): LDS copy (<= 64 tiles) or S.epk
+  std::vector<uint16_t> ewl;  // and its walls (Tables::ewl) for the dual removal test
   uint32_t tr_slot = 0;
   int kt_grid = 0, kt_cap = 16;
   int kt_plan_dw = 0, kt_rs_dw = 0;
@@ -3686,33 +3854,35 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
   // first-use order while adding (x,y)-(x+1,y) and (x,y)-(x,y+1) bidirectionally, x outer, y inner.
   {
     std::vector<int> keys;
-    std::vector<std::vector<int>> dst(c.nt);
+    std::vector<std::vector<std::array<int, 2>>> dst(c.nt);  // (target, direction N/E/S/W)
     std::vector<int> seen(c.nt, 0);
-    auto add1 = [&](int a, int b) {
+    auto add1 = [&](int a, int b, int d) {
       if (!seen[a]) {
         seen[a] = 1;
         keys.push_back(a);
       }
-      dst[a].push_back(b);
+      dst[a].push_back({b, d});
     };
     for (int x = 0; x < tw; x++)
       for (int y = 0; y < th; y++) {
         int t = y * tw + x;
         if (x < tw - 1) {
-          add1(t, t + 1);
-          add1(t + 1, t);
+          add1(t, t + 1, 1);
+          add1(t + 1, t, 3);
         }
         if (y < th - 1) {
-          add1(t, t + tw);
-          add1(t + tw, t);
+          add1(t, t + tw, 2);
+          add1(t + tw, t, 0);
         }
       }
+    // (the direction is recorded, not inferred from the index difference: on a 1-wide map the
+    // southern neighbour t + tw is also t + 1)
     std::vector<int> ea, eb, ed;
     for (int a : keys)
-      for (int b : dst[a]) {
+      for (const auto& bd : dst[a]) {
         ea.push_back(a);
-        eb.push_back(b);
-        ed.push_back(b == a - tw ? 0 : b == a + 1 ? 1 : b == a + tw ? 2 : 3);
+        eb.push_back(bd[0]);
+        ed.push_back(bd[1]);
       }
     const int n = (int)ea.size();
     if (n > kMaxEdges) return fail(h, PGTG_E_UNSUPPORTED, "too many map edges");
@@ -3731,6 +3901,25 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
         d = d == 0 ? 2 : 1;
       }
       h->epk[e] = (uint32_t)a | (uint32_t)b << 8 | (uint32_t)(d == 1 ? 1 : 0) << 16 | (uint32_t)rev << 17;
+    }
+    // the dual test (remove_edges_dual): the wall of each removable edge as two corner codes
+    c.dual = (tw >= 2 && th >= 2 && c.nt <= kSmallTiles && tw + th <= 31) ? 1 : 0;
+    h->ewl.assign(n, 0);
+    if (c.dual) {
+      auto ccode = [&](int cx, int cy) -> int {
+        if (cx >= 1 && cx <= tw - 1 && cy >= 1 && cy <= th - 1) return (cy - 1) * (tw - 1) + (cx - 1);
+        if (cy == 0 && cx < tw) return 64 + cx;                      // north side, clockwise
+        if (cx == tw) return 64 + tw + cy;                          // east side
+        if (cy == th) return 64 + tw + th + (tw - cx);              // south side
+        return 64 + 2 * tw + th + (th - cy);                        // west side
+      };
+      for (int e = 0; e < n; e++) {
+        const uint32_t pk = h->epk[e];
+        const int a = (int)(pk & 255u), ax = a % tw, ay = a / tw;
+        const bool hz = (pk >> 16) & 1u;
+        const int p = hz ? ccode(ax + 1, ay) : ccode(ax, ay + 1), q = ccode(ax + 1, ay + 1);
+        h->ewl[e] = (uint16_t)(p | q << 8);
+      }
     }
     c.keep = (int)nearbyint((double)n * in.pct_connections);  // Python round (half to even)
   }
@@ -3755,6 +3944,18 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
       c.bd[i] = (uint8_t)L[i][2];
     }
     c.n_border_add = (int)nearbyint((double)L.size() * in.pct_connections);
+    if (c.dual) {  // generate_map's dual path maps a candidate index to (tile, direction) by arithmetic
+      bool ok = c.n_border == 2 * tw + 2 * th - 2 && c.n_border < 64;
+      for (int j = 0; ok && j < c.n_border; j++) {
+        int t, d;
+        if (j < tw) { t = j; d = 0; }
+        else if (j < tw + th - 1) { t = (j - tw + 1) * tw + tw - 1; d = 1; }
+        else if (j < 2 * tw + th - 1) { t = (th - 1) * tw + (j - tw - th + 1); d = 2; }
+        else { t = (j - 2 * tw - th + 1) * tw; d = 3; }
+        ok = c.bt[j] == t && c.bd[j] == d;
+      }
+      if (!ok) c.dual = 0;
+    }
   }
   c.obstacle_probability = in.obstacle_probability;
   {
@@ -4141,6 +4342,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     memcpy(t.lanes, hs::kLanes, sizeof t.lanes);
     memcpy(t.ind, c.ind_reward, sizeof t.ind);
     if (c.n_edges <= kSmallEdges) memcpy(t.epk, h->epk.data(), h->epk.size() * sizeof(uint32_t));
+    if (c.n_edges <= kSmallEdges) memcpy(t.ewl, h->ewl.data(), h->ewl.size() * sizeof(uint16_t));
     memcpy(t.bt, c.bt, sizeof t.bt);
     memcpy(t.bd, c.bd, sizeof t.bd);
     for (int k = 0; k < PGTG_MAX_CHANNELS; k++) t.chan[k] = (uint8_t)c.channels[k];
