@@ -175,6 +175,65 @@ def load_latency(workload: str, n_envs: int, avg_kernel_s: float):
             "phases_mean_cycles": d.get("phases_mean_cycles"), "source": p}
 
 
+def adapter_bench(args) -> None:
+    """The reference caller's interface (pgtg/train.py:39-55: TimeLimit(100) -> FlattenObservation ->
+    SubprocVecEnv) served by PGTGSB3VecEnv: K steps of step_async/step_wait with the flattened
+    observation vectors, rewards, dones and infos returned -- as host numpy arrays (SB3's VecEnv
+    contract) or as device tensors (`device_obs=True`).  Actions: uniform random, pre-generated (host
+    array or device tensor).  Not a BASELINE metric; one JSON line."""
+    import numpy as np
+    import torch
+
+    from pgtg_amd.build import build
+    build()
+    from pgtg_amd.sb3 import PGTGSB3VecEnv
+    _, desc, n, kwargs = WORKLOADS["train"]
+    n = args.envs or n
+    kwargs = dict(kwargs)
+    mes = kwargs.pop("max_episode_steps", 100)
+    dev = args.adapter == "device"
+    env = PGTGSB3VecEnv(n, max_episode_steps=mes, device=0, seed=0, device_obs=dev, **kwargs)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(12345)
+    acts = torch.randint(0, 9, (args.warmup + args.steps, n), device="cuda", dtype=torch.uint8, generator=g)
+    host_acts = None if dev else acts.cpu().numpy()
+    a = (lambda t: acts[t]) if dev else (lambda t: host_acts[t])
+    for t in range(args.warmup):
+        env.step(a(t))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done = 0
+    monitor = args.adapter == "host-monitor"
+    ep_ret, ep_len = np.zeros(n), np.zeros(n, np.int64)
+    for t in range(args.warmup, args.warmup + args.steps):
+        obs, rew, dones, infos = env.step(a(t))
+        if monitor:  # stable_baselines3 VecMonitor.step_wait: returns, lengths, list(infos[:]), episode dicts
+            ep_ret += rew
+            ep_len += 1
+            new_infos = list(infos[:])
+            for i in np.nonzero(dones)[0]:
+                info = dict(infos[i])
+                info["episode"] = {"r": ep_ret[i], "l": ep_len[i], "t": 0.0}
+                new_infos[i] = info
+                ep_ret[i] = 0
+                ep_len[i] = 0
+                done += 1
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    rec = {"metric": "env-steps/sec through the SB3 VecEnv adapter (PGTGSB3VecEnv.step_async/step_wait)",
+           "value": n * args.steps / dt, "unit": "env-steps/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True,
+           "path": ("device tensors (device_obs=True): flattened obs, rewards, dones and terminal "
+                    "observations stay in HBM" if dev else
+                    "host numpy (SB3's VecEnv contract): flattened float32 obs copied to the host every step"
+                    + (", plus VecMonitor's per-step host work (list(infos[:]), episode dicts)" if monitor else "")),
+           "obs_dim": env.obs_dim, "obs_bytes_per_step": n * env.obs_dim * 4,
+           "data": "synthetic (uniform random actions, seeds 0..N-1)",
+           "config": {"workload": "caller: " + desc, "envs": n, "adapter": args.adapter}}
+    print(json.dumps(rec), flush=True)
+    env.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,7 +256,13 @@ def main():
     ap.add_argument("--envs-per-block", type=int, default=0, help="A/B: force the step kernel's envs per workgroup")
     ap.add_argument("--kt-wpc", type=int, default=0, help="A/B: k_traffic workgroups per CU")
     ap.add_argument("--kt-cap", type=int, default=0, help="A/B: k_traffic envs per wave held in LDS")
+    ap.add_argument("--adapter", choices=["host", "host-monitor", "device"], default="",
+                    help="time the SB3 VecEnv adapter (pgtg_amd/sb3.py) instead: PGTGSB3VecEnv.step over "
+                         "the caller workload (pgtg/train.py's settings), host numpy or device-tensor path; "
+                         "host-monitor adds SB3 VecMonitor's per-step host work (pgtg/train.py:55)")
     args = ap.parse_args()
+    if args.adapter:
+        return adapter_bench(args)
 
     import torch
     import torch.distributed as dist
@@ -324,9 +389,13 @@ def main():
                                         "MI355X_MICROARCH.md measured float4 copy 6290 GB/s)",
                          "peak_copy_measured": peak_copy,
                          "peak_spec": PEAK_HBM_SPEC_GBS, "frac_spec": achieved / PEAK_HBM_SPEC_GBS,
-                         "kernel": env.step_kernel() + " (step + in-kernel auto-reset)",
+                         "kernel": env.step_kernel() + " (step + in-kernel auto-reset)"
+                                   + (" + k_traffic (initial traffic of the reset envs)" if spec.traffic_density > 0 else ""),
                          "avg_kernel_us": avg_kernel_s * 1e6, "timed_launches": launches,
-                         "kernel_timing": "HIP event pair around the timed window on the launch stream / launches",
+                         "kernel_timing": ("HIP event pair around the timed window on the launch stream / launches"
+                                           + (": device time per step, both kernels" if spec.traffic_density > 0 else "")
+                                           + ("; one host call per step (--per-step): launch gaps included"
+                                              if args.per_step else "")),
                          "alg_bytes_per_launch": alg, "alg_model": "SURVEY.md 8(d)",
                          "resets_per_launch": resets_per_launch, "cars_per_env": cars,
                          "envs_per_workgroup": env.launch_info()[0], "lds_bytes": env.launch_info()[1],

@@ -1717,6 +1717,68 @@ struct BitSink {
   }
 };
 
+template <typename T>
+__device__ __forceinline__ T sel4(int k, T a0, T a1, T a2, T a3) {
+  return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
+}
+
+// One channel's 81 bits (3 words, square lx * 9 + ly) on tile t of the map: the tile tables' algebra of
+// build_obs's one-tile fast path, for any channel code but the lane and spawner ones (square_flags and
+// chan_bit semantics; occ: the tile counters of k_env<true>, null elsewhere).
+template <bool TR, bool BIG>
+__device__ __forceinline__ void tile_chan(const DevCfg& c, const EnvView& v, uint32_t p, int t, int code, int color,
+                                          const uint8_t* occ, uint32_t (&m)[3]) {
+  const uint32_t ex = plan_exits(p), ot = plan_otype(p);
+  const int sd = plan_sgdir(p);
+  const bool used = used_bit<BIG>(v, p, t);
+  const int st_t = (int)(v.sg & 0xffu), st_d = (int)((v.sg >> 8) & 0xffu);
+  const int gl_t = (int)((v.sg >> 16) & 0xffu), gl_d = (int)(v.sg >> 24);
+  const bool sg_on = sd >= 0 && ((ex >> sd) & 1u), fi_on = t == gl_t && ((ex >> gl_d) & 1u);
+  const bool st_on = t == st_t && ((ex >> st_d) & 1u);
+  const uint32_t om = min(plan_omask(p), (uint32_t)PGTG_N_OBST_MASKS - 1u);
+  // the obstacle kind this code shows (ice 1, broken road 2, sand 3, a light of the current colour 4)
+  const uint32_t okind = code == PGTG_CH_ICE ? 1u : code == PGTG_CH_BROKEN ? 2u : code == PGTG_CH_SAND ? 3u
+                       : (code == PGTG_CH_TL_GREEN && color == 0) || (code == PGTG_CH_TL_YELLOW && color == 1) ||
+                         (code == PGTG_CH_TL_RED && color == 2) ? 4u : 0u;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint32_t W3 = sT.wall[ex][k];
+    const uint32_t sgk = sT.seg[sd >= 0 ? sd : 0][k], fik = sT.seg[gl_d & 3][k], stk = sT.seg[st_d & 3][k];
+    const uint32_t obk = sT.obst[om][k] & ~W3;
+    const uint32_t SG = sg_on && !used ? sgk : 0u, US = sg_on && used ? sgk : 0u;
+    const uint32_t FI = fi_on ? fik : 0u, ST = st_on ? stk : 0u;
+    uint32_t val;
+    switch (code) {
+      case PGTG_CH_WALL: val = W3; break;
+      case PGTG_CH_GOALS: val = SG | FI; break;
+      case PGTG_CH_START: val = ST; break;
+      case PGTG_CH_SUBGOAL: val = SG; break;
+      case PGTG_CH_USED_SUBGOAL: val = US; break;
+      case PGTG_CH_FINAL_GOAL: val = FI; break;
+      default: val = (okind != 0u && ot == okind) ? obk : 0u; break;  // obstacles, lights; others zero
+    }
+    m[k] = val;
+  }
+  if (TR && code == PGTG_CH_TRAFFIC) {
+    m[0] = m[1] = m[2] = 0u;
+    if (c.need_car && occ && ex) {
+      const uint32_t* ow = reinterpret_cast<const uint32_t*>(occ + t * 16);  // the tile's 32 nibbles
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        uint32_t nz = (ow[q] | (ow[q] >> 1) | (ow[q] >> 2) | (ow[q] >> 3)) & 0x11111111u;  // nonzero nibbles
+        while (nz) {
+          const int sq = sTX.slot_sq[ex][q * 8 + ((__ffs((int)nz) - 1) >> 2)];
+          nz &= nz - 1u;
+          const uint32_t b = 1u << (sq & 31);
+          m[0] |= (sq >> 5) == 0 ? b : 0u;
+          m[1] |= (sq >> 5) == 1 ? b : 0u;
+          m[2] |= (sq >> 5) == 2 ? b : 0u;
+        }
+      }
+    }
+  }
+}
+
 // Observation of one env into the image at bit offset bit0 (see BitSink): channel by channel, each
 // the window's squares row-major over x, then y.
 // Channels [ch_lo, ch_hi) only (default all) when the lanes of a group share one env's image (the
@@ -1832,6 +1894,62 @@ __device__ __forceinline__ void build_obs(const DevCfg& c, const DevState& S, co
       sink.put(out3[0], 32u);
       sink.put(out3[1], 32u);
       sink.put(out3[2] & 0x1ffffu, 17u);  // 81 = 32 + 32 + 17 bits
+    }
+    if (gap) sink.skip(gap);
+  } else if (TR && c.sliding && !c.generic_channels && c.win <= 11) {
+    // Sliding windows of <= 11 squares (size <= 5) without lane or spawner channels, traffic kernel:
+    // the window touches <= 3 x 3 tiles.  Per channel and tile column, the 81-bit masks of its three
+    // tiles (tile_chan, the fast path's table algebra), then the window rows of that column (one x, the
+    // win y's each) cut from them: 9-bit tile columns placed at their offset, squares outside the map
+    // walls (get_map_cutout's fill, environment.py:1384).  No per-square lookups: the caller workload's
+    // 11 x 11 images were ~45 % of its k_env<true> waves.  The loops are uniform (a row outside this
+    // lane's window is skipped by predication), so that the masks stay in 9 registers.
+    const int win = c.win, x0 = oi.x0, y0 = oi.y0;
+    const int tx0 = max(x0, 0) / kTile, ty0 = max(y0, 0) / kTile;
+    const int txe = min(x0 + win - 1, c.W - 1) / kTile, tye = min(y0 + win - 1, c.H - 1) / kTile;
+    const uint32_t wmask = (1u << win) - 1u;
+    const int lo_out = min(win, max(0, -y0)), hi_in = min(win, max(0, c.H - y0));
+    const uint32_t yfill = ((1u << lo_out) - 1u) | (wmask & ~((1u << hi_in) - 1u));  // y outside the map
+    const int pre = min(win, max(0, -x0)), post = min(win, max(0, x0 + win - c.W));  // rows x < 0, x >= W
+    uint32_t gap = 0;
+    for (int ci = ch_lo; ci < ch_hi; ci++) {
+      const int code = lane_codes ? (int)sT.chan[ci] : c.channels[ci];
+      if (ZS && code < 32 && ((c.zero_ch >> code) & 1u)) {
+        gap += (uint32_t)WW;
+        continue;
+      }
+      if (gap) {
+        sink.skip(gap);
+        gap = 0;
+      }
+      const uint32_t fill = code == PGTG_CH_WALL ? wmask : 0u;
+      for (int i = 0; i < pre; i++) sink.put(fill, (uint32_t)win);
+      for (int a = 0; a < 3; a++) {
+        if (tx0 + a > txe) continue;
+        uint32_t M[3][3];
+#pragma unroll
+        for (int b = 0; b < 3; b++) {
+          const bool ok = ty0 + b <= tye;
+          const int t = ok ? (ty0 + b) * c.tw + tx0 + a : 0;
+          tile_chan<TR, BIG>(c, v, pl[t], t, code, color, occ, M[b]);
+          if (!ok) M[b][0] = M[b][1] = M[b][2] = 0u;
+        }
+        const int xa = (tx0 + a) * kTile;
+        for (int lx = max(0, x0 - xa); lx < min(kTile, x0 + win - xa); lx++) {
+          if (xa + lx >= c.W) break;
+          const int off = lx * kTile, wd = off >> 5, sh = off & 31;
+          uint64_t r64 = 0;
+#pragma unroll
+          for (int b = 0; b < 3; b++) {
+            const uint32_t lo = wd == 0 ? M[b][0] : (wd == 1 ? M[b][1] : M[b][2]), hi = wd == 0 ? M[b][1] : M[b][2];
+            const uint32_t c9 = ((lo >> sh) | (sh ? hi << (32 - sh) : 0u)) & 511u;
+            const int s9 = (ty0 + b) * kTile - y0;
+            r64 |= s9 >= 0 ? (uint64_t)c9 << s9 : (uint64_t)(c9 >> -s9);
+          }
+          sink.put(((uint32_t)r64 & wmask) | (fill & yfill), (uint32_t)win);
+        }
+      }
+      for (int i = 0; i < post; i++) sink.put(fill, (uint32_t)win);
     }
     if (gap) sink.skip(gap);
   } else if (TR && WW <= 128) {
@@ -1983,10 +2101,6 @@ struct BrakeQuery {
 // _spawn_new_car :970-1002).  Survivors keep their slots, respawned cars are appended behind the
 // tail in creation order (slot order = list order); occupancy counters follow every move so later
 // cars see earlier ones.
-template <typename T>
-__device__ __forceinline__ T sel4(int k, T a0, T a1, T a2, T a3) {
-  return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
-}
 
 // The per-car work is organised for a divergent wave: every map lookup the car may need (its slot,
 // the four neighbours, the first admissible one, light and occupancy there) is computed branch-free
@@ -3123,6 +3237,14 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
                               (uint32_t)len | (uint32_t)(-err) << 16, 0u);
 }
 
+// k_envq ablations (tools/ablate.sh): compiled in only in the tuning build; the product kernel tests
+// no runtime flag for them
+#ifdef PGTG_TUNING
+#define ABLATE(L, bit) (((L).abl & (bit)) != 0)
+#else
+#define ABLATE(L, bit) false
+#endif
+
 // Barrier among the waves of a workgroup that take part (lane 0 of each arrives at an LDS counter
 // that only grows; `target` = uses so far x participating waves), for phases that must not wait
 // for a wave busy elsewhere.
@@ -3210,6 +3332,10 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   const int nb = (int)min((uint64_t)L.envs, S.n - env0);
   const int env_waves = (L.envs + 63) / 64, gen_wave = env_waves;
   const bool env_wave = wave < env_waves;
+#if defined(PGTG_ENV_PRIO) && PGTG_ENV_PRIO > 0
+  // (A/B) the env and writer waves ahead of the map-generating wave in VALU arbitration
+  if (wave != gen_wave) __builtin_amdgcn_s_setprio(PGTG_ENV_PRIO);
+#endif
   const int slot = tid;
   const uint64_t i = env0 + slot;
   const bool live = env_wave && slot < nb;
@@ -3278,7 +3404,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       gen_queue_entry<BIG>(c, S, ie, xf[e * L.scratch_dw] + 5u * (uint32_t)l, gplan, pdw,
                       S.qbuf + (ie * kQueueDepth + rslot) * (uint64_t)c.qrec_dw);
     };
-    if (L.abl & 1) {
+    if (ABLATE(L, 1)) {
       if (any_empty) __syncthreads();
       return;
     }
@@ -3337,7 +3463,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   STAMP(28);
   sub_barrier(ctr, bar += (uint32_t)np);
   STAMP(29);
-  if (out.final_obs && !(L.abl & 2))
+  if (out.final_obs && !ABLATE(L, 2))
     write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, rank, nthr, lm);
   STAMP(3);
   sub_barrier(ctr, bar += (uint32_t)np);  // terminal images written before they are rebuilt
@@ -3419,7 +3545,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   STAMP(30);
   sub_barrier(ctr, bar += (uint32_t)np);
   STAMP(31);
-  if (out.obs && !(L.abl & 4))
+  if (out.obs && !ABLATE(L, 4))
     write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr, rank, nthr);
   if (tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
   stagger_record(L, S, t_start);

@@ -38,7 +38,15 @@ def flatten_obs(spec, obs: dict, dtype=None):
     parts = [obs["map"][k].reshape(n, -1).to(dtype) for k in sorted(obs["map"])]
     if spec.next_subgoal:
         parts.append(torch.nn.functional.one_hot(obs["next_subgoal_direction"].long() + 1, 9).to(dtype))
-    parts.append(torch.nn.functional.one_hot(pos[:, 0].clamp(0, 8), 9).to(dtype))
-    parts.append(torch.nn.functional.one_hot(pos[:, 1].clamp(0, 8), 9).to(dtype))
+    # MultiDiscrete([9, 9]): one 18-entry vector with ones at offsets + x = (x, 9 + y).  The position is
+    # the agent's square in its tile (0..8) or, with a sliding window, (s, s) (environment.py:1453), so
+    # a window of size s >= 9 puts 9 + s past the vector's end, where gymnasium's index assignment
+    # raises -- as here, decided from the spec without reading the tensor.
+    if spec.sliding and spec.sliding_size >= 9:
+        raise IndexError(f"position ({spec.sliding_size}, {spec.sliding_size}) is outside MultiDiscrete([9, 9]): "
+                         f"index {9 + spec.sliding_size} is out of bounds for its flattened size 18")
+    oh = torch.zeros((n, 18), dtype=dtype, device=pos.device)
+    oh.scatter_(1, torch.stack([pos[:, 0], 9 + pos[:, 1]], dim=1), 1)
+    parts.append(oh)
     parts.append(obs["velocity"].to(dtype))
     return torch.cat(parts, dim=1)

@@ -9,6 +9,13 @@ Python loop in the step).  Observations are the `FlattenObservation`
 vectors of pgtg/train.py:40 (pgtg_amd/flat.py), as float32 numpy arrays because SB3 policies take
 host arrays; `max_episode_steps` is the `TimeLimit(100)` wrapper of pgtg/train.py:39, applied
 in-kernel (truncation and auto-reset in the same step).
+
+`device_obs=True` keeps everything on the env's GPU for device-side rollout buffers and policies:
+observations, rewards and dones come back as torch tensors (`obs_dtype`: float32 by default; int8 is
+exact as well, every flattened value being a 0/1 one-hot entry or a velocity in Box(-99, 99)),
+actions may be a device tensor, and the infos (`DeviceVecInfos`)
+carry the batch's terminal observations as one [N, D] tensor, converted to SB3's per-env dicts only
+if an entry is read.  Nothing crosses PCIe in the step.
 """
 from __future__ import annotations
 
@@ -24,11 +31,16 @@ from .vector import PGTGVecEnv
 class VecInfos(Sequence):
     """SB3's per-env `infos` list without per-env Python work in the step: the batch's arrays are kept
     and env i's dict ({"terminal_observation", "TimeLimit.truncated"} when it finished, "cost" with
-    separate_reward_cost) is built when it is read, so a step costs O(1) host work whatever the batch
-    size; callers that read every entry pay for what they read."""
+    separate_reward_cost) is built when it is first read and kept, so a step costs O(1) host work
+    whatever the batch size; callers that read every entry pay for what they read (SB3's VecMonitor,
+    which pgtg/train.py:55 wraps around the env, reads them all: `list(infos[:])` per step)."""
 
     def __init__(self, dones, truncated, final, cost):
         self._dones, self._trunc, self._final, self._cost = dones, truncated, final, cost
+        # env i's dict, built on its first read and returned on every later one: SB3 wrappers
+        # (VecNormalize, VecFrameStack, VecTransposeImage) rewrite infos[i]["terminal_observation"] in
+        # place and rely on reading their own value back, as from SubprocVecEnv's list
+        self._cache: dict[int, dict[str, Any]] = {}
 
     def __len__(self) -> int:
         return len(self._dones)
@@ -40,7 +52,10 @@ class VecInfos(Sequence):
             i += len(self)
         if not 0 <= i < len(self):
             raise IndexError(i)
-        d: dict[str, Any] = {}
+        d = self._cache.get(i)
+        if d is not None:
+            return d
+        d = self._cache[i] = {}
         if self._dones[i]:
             d["terminal_observation"] = self._final[i]
             d["TimeLimit.truncated"] = bool(self._trunc[i])
@@ -53,9 +68,36 @@ class VecInfos(Sequence):
         return np.nonzero(self._dones)[0]
 
 
+class DeviceVecInfos(Sequence):
+    """The infos of a `device_obs` step: the batch's tensors on the device (`dones`, `truncated`,
+    `terminal_observation` [N, D] with valid rows where done, `cost`), and SB3's per-env dicts on
+    demand (the first per-env read copies the masks to the host once)."""
+
+    def __init__(self, dones, truncated, final, cost):
+        self.dones, self.truncated, self.terminal_observation, self.cost = dones, truncated, final, cost
+        self._host: VecInfos | None = None
+
+    def _h(self) -> VecInfos:
+        if self._host is None:
+            d = self.dones.cpu().numpy()
+            self._host = VecInfos(d, self.truncated.cpu().numpy(), self.terminal_observation,
+                                  None if self.cost is None else self.cost.cpu().numpy())
+        return self._host
+
+    def __len__(self) -> int:
+        return int(self.dones.shape[0])
+
+    def __getitem__(self, i):
+        return self._h()[i]
+
+    def finished(self):
+        return self._h().finished()
+
+
 class PGTGSB3VecEnv:
     def __init__(self, num_envs: int, map_path: str | None = None, *, max_episode_steps: int | None = 100,
-                 device: int | None = None, seed: int = 0, **kwargs: Any):
+                 device: int | None = None, seed: int = 0, device_obs: bool = False, obs_dtype=None,
+                 **kwargs: Any):
         self.venv = PGTGVecEnv(num_envs, map_path, device=device, autoreset=True,
                                max_episode_steps=max_episode_steps, **kwargs)
         self.spec = self.venv.spec
@@ -63,6 +105,8 @@ class PGTGSB3VecEnv:
         self.obs_dim = flat_dim(self.spec)
         self._seed = seed
         self._actions = None
+        self.device_obs = bool(device_obs)
+        self.obs_dtype = obs_dtype
         try:
             from gymnasium import spaces
             self.observation_space = spaces.Box(low=-99, high=99, shape=(self.obs_dim,), dtype=np.float32)
@@ -76,19 +120,40 @@ class PGTGSB3VecEnv:
         self._seed = 0 if seed is None else int(seed)
         return [self._seed + i for i in range(self.num_envs)]
 
-    def reset(self) -> np.ndarray:
+    def reset(self):
         obs, _ = self.venv.reset(seed=self._seed)
-        return flatten_obs(self.spec, obs).cpu().numpy()
+        flat = flatten_obs(self.spec, obs, dtype=self._dtype())
+        return flat if self.device_obs else flat.cpu().numpy()
+
+    def _dtype(self):
+        import torch
+        if self.obs_dtype is None:
+            return torch.float32
+        return getattr(torch, self.obs_dtype) if isinstance(self.obs_dtype, str) else self.obs_dtype
 
     def step_async(self, actions) -> None:
-        a = np.asarray(actions).reshape(self.num_envs)
+        import torch
+        if isinstance(actions, torch.Tensor) and actions.device.type == "cuda":
+            # device actions: no host round trip and no range check (that would be a device sync per
+            # step); an action outside Discrete(9) is recorded by the kernel per env (error_count())
+            a = actions.reshape(self.num_envs)
+            self._actions = a if a.dtype == torch.uint8 else a.clamp(0, 255).to(torch.uint8)
+            return
+        a = np.asarray(actions.cpu() if isinstance(actions, torch.Tensor) else actions).reshape(self.num_envs)
         if a.size and (a.min() < 0 or a.max() > 8):  # an out-of-space action raises (environment.py:1118)
             raise KeyError(int(a[(a < 0) | (a > 8)][0]))
-        self._actions = a.astype(np.uint8)
+        self._actions = torch.as_tensor(a.astype(np.uint8))
 
     def step_wait(self):
         import torch
-        obs, reward, term, trunc, infos = self.venv.step(torch.as_tensor(self._actions))
+        obs, reward, term, trunc, infos = self.venv.step(self._actions)
+        if self.device_obs:
+            dt = self._dtype()
+            dones = term.bool() | trunc.bool()
+            final = flatten_obs(self.spec, infos["final_observation"], dtype=dt)  # every row: no sync
+            cost = infos.get("cost")
+            return (flatten_obs(self.spec, obs, dtype=dt), reward.to(torch.float32), dones,
+                    DeviceVecInfos(dones, trunc.bool() & ~term.bool(), final, cost))
         flat = flatten_obs(self.spec, obs).cpu().numpy()
         rew = reward.to(torch.float32).cpu().numpy()
         term_h, trunc_h = term.cpu().numpy().astype(bool), trunc.cpu().numpy().astype(bool)

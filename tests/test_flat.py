@@ -55,3 +55,30 @@ def test_flatten_matches_gymnasium_order(kw):
         if spec.next_subgoal:
             oi["next_subgoal_direction"] = int(obs["next_subgoal_direction"][i])
         assert np.array_equal(flat[i], _gym_flatten(oi, spec))
+
+
+@pytest.mark.parametrize("size", [5, 8, 9, 12])
+def test_sliding_position_offsets(size):
+    """position (s, s) of a sliding window (environment.py:1453) under MultiDiscrete([9, 9])'s flatten:
+    ones at s and 9 + s while they fit the 18 entries; gymnasium's assignment raises IndexError past
+    them (s >= 9), so does flatten_obs (no clamping)."""
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        spec = cfg.make_spec(use_sliding_observation_window=True, sliding_observation_window_size=size)
+    N, w = 3, spec.window
+    obs = {"map": {k: torch.zeros((N, w, w), dtype=torch.uint8) for k, _ in spec.channels},
+           "position": torch.full((N, 2), size, dtype=torch.int32),
+           "velocity": torch.zeros((N, 2), dtype=torch.int32)}
+    if size >= 9:
+        with pytest.raises(IndexError):
+            flatten_obs(spec, obs)
+        oh = np.zeros(18)
+        with pytest.raises(IndexError):  # numpy's behaviour on gymnasium's offsets + x
+            oh[np.array([0, 9]) + np.array([size, size])] = 1
+        return
+    flat = flatten_obs(spec, obs).numpy()
+    pos = flat[:, -20:-2]
+    assert (pos.sum(1) == 2).all() and (pos[:, size] == 1).all() and (pos[:, 9 + size] == 1).all()
+    oi = {"map": {k: obs["map"][k][0].numpy() for k, _ in spec.channels}, "position": obs["position"][0].numpy(),
+          "velocity": obs["velocity"][0].numpy()}
+    assert np.array_equal(flat[0], _gym_flatten(oi, spec))

@@ -105,6 +105,40 @@ def test_sb3_adapter_flattened_obs_and_terminal_infos():
     env.close()
 
 
+def test_sb3_adapter_device_path_equals_host_path():
+    """device_obs=True (pgtg_amd/sb3.py): the same flattened observations, rewards, dones and terminal
+    observations as the host path, as device tensors, with device actions; SB3's per-env infos on
+    demand.  The caller workload's settings (pgtg/train.py:21-40) on 64 envs."""
+    from pgtg_amd.sb3 import PGTGSB3VecEnv
+    kw = dict(random_map_width=4, random_map_height=4, random_map_obstacle_probability=0.2,
+              random_map_percentage_of_connections=0.8, traffic_density=0.2, use_sliding_observation_window=True,
+              sliding_observation_window_size=5, use_next_subgoal_direction=True)
+    N, L = 64, 7
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        host = PGTGSB3VecEnv(N, max_episode_steps=L, seed=3, **kw)
+        dev = PGTGSB3VecEnv(N, max_episode_steps=L, seed=3, device_obs=True, **kw)
+    o_h, o_d = host.reset(), dev.reset()
+    assert isinstance(o_d, torch.Tensor) and o_d.is_cuda and np.array_equal(o_h, o_d.cpu().numpy())
+    g = torch.Generator(device="cuda").manual_seed(1)
+    finished = 0
+    for t in range(25):
+        a = torch.randint(0, 9, (N,), device="cuda", dtype=torch.int64, generator=g)
+        o_h, r_h, d_h, i_h = host.step(a.cpu().numpy())
+        o_d, r_d, d_d, i_d = dev.step(a)
+        assert o_d.is_cuda and r_d.is_cuda and d_d.is_cuda
+        assert np.array_equal(o_h, o_d.cpu().numpy()), t
+        assert np.array_equal(r_h, r_d.cpu().numpy()) and np.array_equal(d_h, d_d.cpu().numpy()), t
+        term = i_d.terminal_observation.cpu().numpy()
+        for i in np.nonzero(d_h)[0]:
+            assert np.array_equal(i_h[i]["terminal_observation"], term[i])
+            assert i_d[i]["TimeLimit.truncated"] == i_h[i]["TimeLimit.truncated"]
+            finished += 1
+    assert finished > 0
+    host.close()
+    dev.close()
+
+
 def test_sharded_batch_equals_the_global_batch():
     """bench/dist sharding: rank r's envs are seeded with r*n_local + i, so two half batches step
     exactly like the global batch (pgtg_amd/dist.py)."""

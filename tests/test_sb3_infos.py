@@ -32,3 +32,17 @@ def test_vecinfos_matches_the_eager_list():
     with pytest.raises(IndexError):
         inf[n]
     assert VecInfos(np.zeros(3, bool), np.zeros(3, bool), None, None)[2] == {}
+
+
+def test_vecinfos_entries_persist_in_place_edits():
+    """SB3's VecNormalize/VecFrameStack rewrite infos[i]["terminal_observation"] in place and read it
+    back: the sequence must hand out the same dict each time."""
+    dones = np.array([1, 0, 1], bool)
+    final = np.ones((3, 4), np.float32)
+    inf = VecInfos(dones, np.zeros(3, bool), final, None)
+    x = np.full(4, 7.0, np.float32)
+    inf[0]["terminal_observation"] = x
+    assert inf[0]["terminal_observation"] is x and inf[0] is inf[0]
+    assert inf[:1][0]["terminal_observation"] is x and list(inf)[0] is inf[0]
+    inf[-1]["extra"] = 1
+    assert inf[2]["extra"] == 1

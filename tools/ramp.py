@@ -20,7 +20,9 @@ def main():
     _, _, n, kw = bench.WORKLOADS[wl]
     if len(sys.argv) > 3:
         n = int(sys.argv[3])
-    env = PGTGVecEnv(n, spec=make_spec(**kw), device=0, autoreset=True)
+    kw = dict(kw)
+    mes = kw.pop("max_episode_steps", None)  # the TimeLimit wrapper: a PGTGVecEnv argument, not a PGTGEnv kwarg
+    env = PGTGVecEnv(n, spec=make_spec(**kw), device=0, autoreset=True, max_episode_steps=mes)
     acts = None
     rows = []
     for rep in range(2):
