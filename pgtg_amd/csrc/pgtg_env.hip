@@ -741,38 +741,59 @@ __device__ __forceinline__ void remove_edges_dual(const DevCfg& c, const uint32_
   M RH = 0, RV = 0;          // removed tile edges: RH bit a = a|a+1 (horizontal), RV bit a = a|a+w
   CM RA = 0, RB = 0;         // interior corners wall-connected to arc A / arc B
   CM WE = 0, WS = 0;         // interior walls: WE bit k = corner k - k+1, WS bit k = corner k - k+wi
+  // The list index of iteration j is a Lemire draw below n_edges - 2j whatever the outcomes, so the
+  // draws of a batch of 8 iterations come first (a chain of their own, off the list's), then the list
+  // and wall tests consume them; a loop that ends inside a batch replays the draws it used, leaving
+  // the stream where the reference leaves it.
   while (count > keep && nrem > 0) {
-    const int k = (int)pcg_draw(r, true, (uint32_t)nrem);  // nrem >= 2: always draws
-    const int e = L.select(k);
-    const uint32_t pk = epk[e], wl = ewl[e];
-    L.clear(e);
-    L.clear((int)(pk >> 17));
-    nrem -= 2;
-    const int p = (int)(wl & 255u), q = (int)(wl >> 8);
-    const bool ap = corner_in<CM>(p, RA, da.ba), aq = corner_in<CM>(q, RA, da.ba);
-    const bool bp = corner_in<CM>(p, RB, da.bb), bq = corner_in<CM>(q, RB, da.bb);
-    if ((ap && bq) || (bp && aq)) continue;  // the wall would separate s from g: removal undone
-    count -= 2;
-    const bool hz = (pk >> 16) & 1u;
-    const M ma = (M)1 << (pk & (sizeof(M) * 8 - 1));
-    RH |= hz ? ma : (M)0;
-    RV |= hz ? (M)0 : ma;
-    if (ap != aq || bp != bq) {  // the wall attaches the other corner's component to an arc
-      const bool toA = ap != aq;
-      const int o = (toA ? ap : bp) ? q : p;  // interior (a boundary corner's side is fixed)
-      CM C = (CM)1 << (o & (int)(sizeof(CM) * 8 - 1)), N;
-      for (;;) {
-        N = C | ((C & WE) << 1) | ((C >> 1) & WE) | ((C & WS) << wi) | ((C >> wi) & WS);
-        if (N == C) break;
-        C = N;
-      }
-      RA |= toA ? C : (CM)0;
-      RB |= toA ? (CM)0 : C;
+    const Pcg rb = r;
+    const int n0 = nrem;
+    uint32_t kw0 = 0, kw1 = 0;  // 8-bit list indices (n_edges <= 224)
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const int n = n0 - 2 * b;  // wave-uniform
+      const uint32_t k = n >= 2 ? (uint32_t)pcg_draw(r, true, (uint32_t)n) : 0u;
+      if (b < 4) kw0 |= k << (8 * b);
+      else kw1 |= k << (8 * (b - 4));
     }
-    if ((p | q) < 64) {  // interior wall (the component floods above ran without it)
-      const CM wb = (CM)1 << (min(p, q) & (int)(sizeof(CM) * 8 - 1));
-      WS |= hz ? wb : (CM)0;
-      WE |= hz ? (CM)0 : wb;
+    int b = 0;
+    for (; b < 8 && count > keep && nrem > 0; b++) {
+      const int k = (int)(((b < 4 ? kw0 : kw1) >> (8 * (b & 3))) & 255u);
+      const int e = L.select(k);
+      const uint32_t pk = epk[e], wl = ewl[e];
+      L.clear(e);
+      L.clear((int)(pk >> 17));
+      nrem -= 2;
+      const int p = (int)(wl & 255u), q = (int)(wl >> 8);
+      const bool ap = corner_in<CM>(p, RA, da.ba), aq = corner_in<CM>(q, RA, da.ba);
+      const bool bp = corner_in<CM>(p, RB, da.bb), bq = corner_in<CM>(q, RB, da.bb);
+      if ((ap && bq) || (bp && aq)) continue;  // the wall would separate s from g: removal undone
+      count -= 2;
+      const bool hz = (pk >> 16) & 1u;
+      const M ma = (M)1 << (pk & (sizeof(M) * 8 - 1));
+      RH |= hz ? ma : (M)0;
+      RV |= hz ? (M)0 : ma;
+      if (ap != aq || bp != bq) {  // the wall attaches the other corner's component to an arc
+        const bool toA = ap != aq;
+        const int o = (toA ? ap : bp) ? q : p;  // interior (a boundary corner's side is fixed)
+        CM C = (CM)1 << (o & (int)(sizeof(CM) * 8 - 1)), N;
+        for (;;) {
+          N = C | ((C & WE) << 1) | ((C >> 1) & WE) | ((C & WS) << wi) | ((C >> wi) & WS);
+          if (N == C) break;
+          C = N;
+        }
+        RA |= toA ? C : (CM)0;
+        RB |= toA ? (CM)0 : C;
+      }
+      if ((p | q) < 64) {  // interior wall (the component floods above ran without it)
+        const CM wb = (CM)1 << (min(p, q) & (int)(sizeof(CM) * 8 - 1));
+        WS |= hz ? wb : (CM)0;
+        WE |= hz ? (CM)0 : wb;
+      }
+    }
+    if (b < 8) {  // ended inside the batch after b draws
+      r = rb;
+      for (int j = 0; j < b; j++) (void)pcg_draw(r, true, (uint32_t)(n0 - 2 * j));
     }
   }
   hE &= ~RH;
@@ -2734,7 +2755,10 @@ struct Lds {
                        // traffic region; the agent tile's counters and the reset hand-over words in hist
   int abl;             // diagnostic ablations (PGTG_TUNING builds only, PGTG_ABL; always 0 otherwise):
                        // k_envq bit 0 no ring refills, bit 1 no terminal-observation writes, bit 2 no
-                       // observation writes (timing experiments: the results are wrong)
+                       // observation writes, bit 3 the helper spins `spin` dependent VALU steps instead
+                       // of refilling, bit 4 refills without the ring-entry stores (timing experiments:
+                       // the results are wrong)
+  int spin;
 };
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
 constexpr uint64_t kStaggerMaxTicks = 20000;  // 200 us of 100 MHz wall clock: a bound, never reached
@@ -2769,8 +2793,10 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.stagger_wgs = 0;
   l.img_in_traf = 0;
   l.abl = 0;
+  l.spin = 0;
 #ifdef PGTG_TUNING  // A/B and diagnostic builds only: the product library reads no environment
   if (const char* e = getenv("PGTG_ABL")) l.abl = atoi(e);
+  if (const char* e = getenv("PGTG_SPIN")) l.spin = atoi(e);
   if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);
   if (const char* e = getenv("PGTG_COMPACT")) l.compact = atoi(e);
   if (const char* e = getenv("PGTG_QUEUE")) l.queue = l.queue && atoi(e);
@@ -3196,7 +3222,8 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
 // built in the lane's LDS plan scratch and written to HBM.
 template <bool BIG>
 __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState& S, uint64_t i, uint32_t k,
-                                                uint16_t* plan, int pdw, uint32_t* __restrict__ dst) {
+                                                uint16_t* plan, int pdw, uint32_t* __restrict__ dst,
+                                                bool no_store = false) {
   SeedPool sp = ss_pool(S.seed[i]);
   Pcg map_rng = ss_child(sp, k);
   int st_t, st_d, gl_t, gl_d;
@@ -3222,6 +3249,12 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
   const uint32_t* pw = reinterpret_cast<const uint32_t*>(plan);
   uint4* d4 = reinterpret_cast<uint4*>(dst);
   const int pwords = c.plan_stride / 2;
+#ifdef PGTG_TUNING
+  if (no_store) {  // (timing experiment: the entry is built but not written)
+    if (len == 12345 && px == 7) d4[0] = make_uint4(0, 0, 0, 0);
+    return;
+  }
+#endif
   for (int q = 0; q < pwords / 4; q++) {
     uint32_t wv[4];
 #pragma unroll
@@ -3331,6 +3364,9 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
   const int nb = (int)min((uint64_t)L.envs, S.n - env0);
   const int env_waves = (L.envs + 63) / 64, gen_wave = env_waves;
+  // ring entries of levels 1.. regenerated per launch: one per helper lane, two with three env waves
+  // (192 envs reset ~80 times per launch at configs[4]'s rate)
+  const int qcap = env_waves > 2 ? 2 * kQueueLanes : kQueueLanes;
   const bool env_wave = wave < env_waves;
 #if defined(PGTG_ENV_PRIO) && PGTG_ENV_PRIO > 0
   // (A/B) the env and writer waves ahead of the map-generating wave in VALU arbitration
@@ -3402,26 +3438,35 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       const uint32_t qe = xf[e * L.scratch_dw + 1];
       const uint32_t rslot = (((qe >> 2) & 3u) + (uint32_t)l) % (uint32_t)kQueueDepth;
       gen_queue_entry<BIG>(c, S, ie, xf[e * L.scratch_dw] + 5u * (uint32_t)l, gplan, pdw,
-                      S.qbuf + (ie * kQueueDepth + rslot) * (uint64_t)c.qrec_dw);
+                      S.qbuf + (ie * kQueueDepth + rslot) * (uint64_t)c.qrec_dw, ABLATE(L, 16));
     };
     if (ABLATE(L, 1)) {
       if (any_empty) __syncthreads();
       return;
     }
+#ifdef PGTG_TUNING
+    if (ABLATE(L, 8)) {  // issue without memory: a dependent VALU chain as long as a fill
+      uint32_t x = (uint32_t)tid;
+      for (int k = 0; k < L.spin; k++) x = x * 0x9e3779b1u + (x >> 7);
+      if (any_empty) __syncthreads();
+      if (x == 0x12345u) S.err[env0] = 9;
+      return;
+    }
+#endif
     for (int k = lane; k < F[0]; k += kQueueLanes) refill(k, 0);  // every empty ring's head
     if (any_empty) __syncthreads();  // head refills visible to the other waves
-    {
-      int k = lane, l = 1;
+    for (int k0 = lane; k0 < qcap; k0 += kQueueLanes) {  // levels 1.. in list order, up to qcap entries
+      int k = k0, l = 1;
       while (l < kQueueDepth && k >= F[l]) {
         k -= F[l];
         l++;
       }
       if (l < kQueueDepth) refill(k, l);
     }
-    if (lane == 0) {  // maps generated (S.counters[2]): the heads, then one per lane for levels 1..
+    if (lane == 0) {  // maps generated (S.counters[2]): the heads, then up to qcap for levels 1..
       int rest = 0;
       for (int l = 1; l < kQueueDepth; l++) rest += F[l];
-      atomicAdd(&S.counters[2], (unsigned long long)(F[0] + min(rest, kQueueLanes)));
+      atomicAdd(&S.counters[2], (unsigned long long)(F[0] + min(rest, qcap)));
     }
     STAMP(7);
     return;
@@ -3529,7 +3574,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     for (int l = 1; l < kQueueDepth; l++) {
       int pre = 0;
       for (int w = 0; w < wave; w++) pre += __popcll(fm[l * 3 + w]);
-      if (qn <= (uint32_t)l && base + pre + __popcll(fm[l * 3 + wave] & ((1ull << lane) - 1ull)) < kQueueLanes) have++;
+      if (qn <= (uint32_t)l && base + pre + __popcll(fm[l * 3 + wave] & ((1ull << lane) - 1ull)) < qcap) have++;
       base += F[l];
     }
     const uint32_t nq = reset_now ? have - 1u : have;  // have >= 1: every head is refilled
@@ -4255,7 +4300,8 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
            : n_envs <= (uint64_t)64 * 1024 ? 64
            : (n_envs <= (uint64_t)128 * 1024 || queue_able) ? 128 : kBlock;
   if (h->tune_epb) envs = h->tune_epb;
-  if (envs != 16 && envs != 32 && envs != 64 && envs != 128 && envs != kBlock) envs = kBlock;
+  if (envs != 16 && envs != 32 && envs != 64 && envs != 128 && envs != 192 && envs != kBlock) envs = kBlock;
+  if (envs == 192 && !queue_able) envs = kBlock;  // (three env waves and a map-generating one: k_envq only)
   while (envs > 16 && lds_bytes(lds_layout(c, envs)) + sizeof(Tables) > 150 * 1024) envs /= 2;
   h->L = lds_layout(c, envs);
   if (c.need_car) {

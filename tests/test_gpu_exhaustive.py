@@ -110,6 +110,10 @@ CASES = {
                          dict(envs_per_block=256, obs_sub=32)),
     "cfg5_wg256": (65536, 20, dict(random_map_width=5, random_map_height=5), dict(envs_per_block=256)),
     "cfg5_wg64": (20000, 20, dict(random_map_width=5, random_map_height=5), dict(envs_per_block=64)),
+    # map queue with three env waves (192 envs per workgroup, two ring refills per helper lane), past
+    # the rings' first turnover (40 steps) and with a ragged last workgroup
+    "cfg5_wg192": (100000, 40, dict(random_map_width=5, random_map_height=5), dict(envs_per_block=192)),
+    "cfg2_wg192": (30000, 40, dict(random_map_width=3, random_map_height=4), dict(envs_per_block=192)),
     "obstacles_wg32_sub8": (3000, 20, dict(random_map_width=4, random_map_height=4, random_map_obstacle_probability=1.0,
                                            standing_still_penalty=1.0), dict(envs_per_block=32, obs_sub=8)),
 }
