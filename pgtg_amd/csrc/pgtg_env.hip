@@ -741,59 +741,38 @@ __device__ __forceinline__ void remove_edges_dual(const DevCfg& c, const uint32_
   M RH = 0, RV = 0;          // removed tile edges: RH bit a = a|a+1 (horizontal), RV bit a = a|a+w
   CM RA = 0, RB = 0;         // interior corners wall-connected to arc A / arc B
   CM WE = 0, WS = 0;         // interior walls: WE bit k = corner k - k+1, WS bit k = corner k - k+wi
-  // The list index of iteration j is a Lemire draw below n_edges - 2j whatever the outcomes, so the
-  // draws of a batch of 8 iterations come first (a chain of their own, off the list's), then the list
-  // and wall tests consume them; a loop that ends inside a batch replays the draws it used, leaving
-  // the stream where the reference leaves it.
   while (count > keep && nrem > 0) {
-    const Pcg rb = r;
-    const int n0 = nrem;
-    uint32_t kw0 = 0, kw1 = 0;  // 8-bit list indices (n_edges <= 224)
-#pragma unroll
-    for (int b = 0; b < 8; b++) {
-      const int n = n0 - 2 * b;  // wave-uniform
-      const uint32_t k = n >= 2 ? (uint32_t)pcg_draw(r, true, (uint32_t)n) : 0u;
-      if (b < 4) kw0 |= k << (8 * b);
-      else kw1 |= k << (8 * (b - 4));
-    }
-    int b = 0;
-    for (; b < 8 && count > keep && nrem > 0; b++) {
-      const int k = (int)(((b < 4 ? kw0 : kw1) >> (8 * (b & 3))) & 255u);
-      const int e = L.select(k);
-      const uint32_t pk = epk[e], wl = ewl[e];
-      L.clear(e);
-      L.clear((int)(pk >> 17));
-      nrem -= 2;
-      const int p = (int)(wl & 255u), q = (int)(wl >> 8);
-      const bool ap = corner_in<CM>(p, RA, da.ba), aq = corner_in<CM>(q, RA, da.ba);
-      const bool bp = corner_in<CM>(p, RB, da.bb), bq = corner_in<CM>(q, RB, da.bb);
-      if ((ap && bq) || (bp && aq)) continue;  // the wall would separate s from g: removal undone
-      count -= 2;
-      const bool hz = (pk >> 16) & 1u;
-      const M ma = (M)1 << (pk & (sizeof(M) * 8 - 1));
-      RH |= hz ? ma : (M)0;
-      RV |= hz ? (M)0 : ma;
-      if (ap != aq || bp != bq) {  // the wall attaches the other corner's component to an arc
-        const bool toA = ap != aq;
-        const int o = (toA ? ap : bp) ? q : p;  // interior (a boundary corner's side is fixed)
-        CM C = (CM)1 << (o & (int)(sizeof(CM) * 8 - 1)), N;
-        for (;;) {
-          N = C | ((C & WE) << 1) | ((C >> 1) & WE) | ((C & WS) << wi) | ((C >> wi) & WS);
-          if (N == C) break;
-          C = N;
-        }
-        RA |= toA ? C : (CM)0;
-        RB |= toA ? (CM)0 : C;
+    const int k = (int)pcg_draw(r, true, (uint32_t)nrem);  // nrem >= 2: always draws
+    const int e = L.select(k);
+    const uint32_t pk = epk[e], wl = ewl[e];
+    L.clear(e);
+    L.clear((int)(pk >> 17));
+    nrem -= 2;
+    const int p = (int)(wl & 255u), q = (int)(wl >> 8);
+    const bool ap = corner_in<CM>(p, RA, da.ba), aq = corner_in<CM>(q, RA, da.ba);
+    const bool bp = corner_in<CM>(p, RB, da.bb), bq = corner_in<CM>(q, RB, da.bb);
+    if ((ap && bq) || (bp && aq)) continue;  // the wall would separate s from g: removal undone
+    count -= 2;
+    const bool hz = (pk >> 16) & 1u;
+    const M ma = (M)1 << (pk & (sizeof(M) * 8 - 1));
+    RH |= hz ? ma : (M)0;
+    RV |= hz ? (M)0 : ma;
+    if (ap != aq || bp != bq) {  // the wall attaches the other corner's component to an arc
+      const bool toA = ap != aq;
+      const int o = (toA ? ap : bp) ? q : p;  // interior (a boundary corner's side is fixed)
+      CM C = (CM)1 << (o & (int)(sizeof(CM) * 8 - 1)), N;
+      for (;;) {
+        N = C | ((C & WE) << 1) | ((C >> 1) & WE) | ((C & WS) << wi) | ((C >> wi) & WS);
+        if (N == C) break;
+        C = N;
       }
-      if ((p | q) < 64) {  // interior wall (the component floods above ran without it)
-        const CM wb = (CM)1 << (min(p, q) & (int)(sizeof(CM) * 8 - 1));
-        WS |= hz ? wb : (CM)0;
-        WE |= hz ? (CM)0 : wb;
-      }
+      RA |= toA ? C : (CM)0;
+      RB |= toA ? (CM)0 : C;
     }
-    if (b < 8) {  // ended inside the batch after b draws
-      r = rb;
-      for (int j = 0; j < b; j++) (void)pcg_draw(r, true, (uint32_t)(n0 - 2 * j));
+    if ((p | q) < 64) {  // interior wall (the component floods above ran without it)
+      const CM wb = (CM)1 << (min(p, q) & (int)(sizeof(CM) * 8 - 1));
+      WS |= hz ? wb : (CM)0;
+      WE |= hz ? (CM)0 : wb;
     }
   }
   hE &= ~RH;
