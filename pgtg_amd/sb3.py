@@ -7,7 +7,8 @@ pgtg/train.py:54-55).
 `infos[i]["TimeLimit.truncated"]` for finished envs (`infos` a lazy sequence, `VecInfos`: no per-env
 Python loop in the step).  Observations are the `FlattenObservation`
 vectors of pgtg/train.py:40 (pgtg_amd/flat.py), as float32 numpy arrays because SB3 policies take
-host arrays; `max_episode_steps` is the `TimeLimit(100)` wrapper of pgtg/train.py:39, applied
+host arrays (views of two page-locked buffer sets used in turn: a step's arrays are valid until the
+step after next -- SB3's rollout buffer copies them at once); `max_episode_steps` is the `TimeLimit(100)` wrapper of pgtg/train.py:39, applied
 in-kernel (truncation and auto-reset in the same step).
 
 `device_obs=True` keeps everything on the env's GPU for device-side rollout buffers and policies:
@@ -35,32 +36,56 @@ class VecInfos(Sequence):
     whatever the batch size; callers that read every entry pay for what they read (SB3's VecMonitor,
     which pgtg/train.py:55 wraps around the env, reads them all: `list(infos[:])` per step)."""
 
-    def __init__(self, dones, truncated, final, cost):
+    def __init__(self, dones, truncated, final, cost, final_rows=None):
+        """final: the terminal observations, one row per env ([N, D]), or with `final_rows` one row per
+        finished env in env order (final_rows[i] = env i's row)."""
         self._dones, self._trunc, self._final, self._cost = dones, truncated, final, cost
+        self._rows = final_rows
         # env i's dict, built on its first read and returned on every later one: SB3 wrappers
         # (VecNormalize, VecFrameStack, VecTransposeImage) rewrite infos[i]["terminal_observation"] in
         # place and rely on reading their own value back, as from SubprocVecEnv's list
         self._cache: dict[int, dict[str, Any]] = {}
+        self._all: list | None = None
 
     def __len__(self) -> int:
         return len(self._dones)
 
+    def _make(self, i: int) -> dict[str, Any]:
+        d: dict[str, Any] = {}
+        if self._dones[i]:
+            d["terminal_observation"] = self._final[i if self._rows is None else int(self._rows[i])]
+            d["TimeLimit.truncated"] = bool(self._trunc[i])
+        if self._cost is not None:
+            d["cost"] = float(self._cost[i])
+        return d
+
+    def _materialize(self) -> list:
+        """Every entry at once (VecMonitor's list(infos[:])): plain dicts, then the finished envs'."""
+        if self._all is None:
+            n = len(self)
+            if self._cost is None:
+                lst = [{} for _ in range(n)]
+            else:
+                lst = [{"cost": c} for c in self._cost.tolist()]
+            for i in np.nonzero(self._dones)[0].tolist():
+                lst[i].update(self._make(i))
+            for i, d in self._cache.items():  # entries already handed out stay the same objects
+                lst[i] = d
+            self._all = lst
+        return self._all
+
     def __getitem__(self, i):
         if isinstance(i, slice):
-            return [self[k] for k in range(*i.indices(len(self)))]
+            return self._materialize()[i]
         if i < 0:
             i += len(self)
         if not 0 <= i < len(self):
             raise IndexError(i)
+        if self._all is not None:
+            return self._all[i]
         d = self._cache.get(i)
-        if d is not None:
-            return d
-        d = self._cache[i] = {}
-        if self._dones[i]:
-            d["terminal_observation"] = self._final[i]
-            d["TimeLimit.truncated"] = bool(self._trunc[i])
-        if self._cost is not None:
-            d["cost"] = float(self._cost[i])
+        if d is None:
+            d = self._cache[i] = self._make(i)
         return d
 
     def finished(self) -> np.ndarray:
@@ -154,13 +179,45 @@ class PGTGSB3VecEnv:
             cost = infos.get("cost")
             return (flatten_obs(self.spec, obs, dtype=dt), reward.to(torch.float32), dones,
                     DeviceVecInfos(dones, trunc.bool() & ~term.bool(), final, cost))
-        flat = flatten_obs(self.spec, obs).cpu().numpy()
-        rew = reward.to(torch.float32).cpu().numpy()
-        term_h, trunc_h = term.cpu().numpy().astype(bool), trunc.cpu().numpy().astype(bool)
+        # host arrays (SB3's VecEnv contract): one copy per step into page-locked buffers, two sets used
+        # in turn (the arrays a step returns stay valid through the next step), and the terminal
+        # observations of the finished envs only
+        h = self._host_buffers()
+        flat_d = flatten_obs(self.spec, obs)
+        h["obs"].copy_(flat_d, non_blocking=True)
+        h["rew"].copy_(reward.to(torch.float32), non_blocking=True)
+        h["term"].copy_(term, non_blocking=True)
+        h["trunc"].copy_(trunc, non_blocking=True)
+        cost = None
+        if "cost" in infos:
+            h["cost"].copy_(infos["cost"], non_blocking=True)
+        torch.cuda.current_stream(self.venv.device).synchronize()
+        term_h, trunc_h = h["term"].numpy().astype(bool), h["trunc"].numpy().astype(bool)
         dones = term_h | trunc_h
-        final = flatten_obs(self.spec, infos["final_observation"]).cpu().numpy() if dones.any() else None
-        cost = infos["cost"].cpu().numpy() if "cost" in infos else None
-        return flat, rew, dones, VecInfos(dones, trunc_h & ~term_h, final, cost)
+        final, rows = None, None
+        idx = np.nonzero(dones)[0]
+        if idx.size:
+            fin = flatten_obs(self.spec, infos["final_observation"])
+            final = fin.index_select(0, torch.as_tensor(idx, device=fin.device)).cpu().numpy()
+            rows = np.full(self.num_envs, -1, np.int64)
+            rows[idx] = np.arange(idx.size)
+        if "cost" in infos:
+            cost = h["cost"].numpy().copy()
+        return h["obs"].numpy(), h["rew"].numpy(), dones, VecInfos(dones, trunc_h & ~term_h, final, cost, rows)
+
+    def _host_buffers(self) -> dict:
+        import torch
+        if not hasattr(self, "_hbuf"):
+            def pinned(shape, dtype):
+                return torch.empty(shape, dtype=dtype, pin_memory=True)
+            self._hbuf = [{"obs": pinned((self.num_envs, self.obs_dim), torch.float32),
+                           "rew": pinned((self.num_envs,), torch.float32),
+                           "term": pinned((self.num_envs,), torch.uint8),
+                           "trunc": pinned((self.num_envs,), torch.uint8),
+                           "cost": pinned((self.num_envs,), torch.float64)} for _ in range(2)]
+            self._flip = 0
+        self._flip ^= 1
+        return self._hbuf[self._flip]
 
     def step(self, actions):
         self.step_async(actions)

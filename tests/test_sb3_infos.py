@@ -46,3 +46,19 @@ def test_vecinfos_entries_persist_in_place_edits():
     assert inf[:1][0]["terminal_observation"] is x and list(inf)[0] is inf[0]
     inf[-1]["extra"] = 1
     assert inf[2]["extra"] == 1
+
+
+def test_vecinfos_finished_rows_and_full_reads():
+    """Terminal observations stored one row per finished env (final_rows), and VecMonitor's
+    list(infos[:]) (pgtg/train.py:55) giving the same dict objects as per-env reads, before and after."""
+    dones = np.array([0, 1, 0, 0, 1], bool)
+    rows = np.array([-1, 0, -1, -1, 1])
+    final = np.array([[1.0, 2.0], [3.0, 4.0]], np.float32)
+    cost = np.array([0.5, 0.0, 1.0, 2.0, 0.25])
+    inf = VecInfos(dones, np.zeros(5, bool), final, cost, rows)
+    first = inf[4]
+    allv = list(inf[:])
+    assert allv[4] is first and inf[4] is first and inf[1] is allv[1]
+    assert np.array_equal(allv[1]["terminal_observation"], final[0]) and np.array_equal(first["terminal_observation"], final[1])
+    assert allv[0] == {"cost": 0.5} and allv[3] == {"cost": 2.0} and allv[1]["cost"] == 0.0
+    assert len(inf[1:3]) == 2 and inf[-1] is first

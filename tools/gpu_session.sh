@@ -11,6 +11,7 @@
 #   benchlong:<wl>   bench.py --workload <wl> with the default 1000-step window
 #   rccl             bench.py under torch.distributed.run, one rank, nccl backend, --dist (RCCL init +
 #                    the device counter all-reduce), 131 072 envs
+#   ranks            2 and 4 ranks on one GPU (gloo) at the full configs[4] batch, per-env digests vs one process
 #   shards           single-process lines at the per-rank shards of N = 2, 4, 8 (524 288 / 262 144 /
 #                    131 072 envs) beside the 1 048 576-env line
 #   profile:<wl,..>  tools/gpu_profile.sh (rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes)
@@ -62,6 +63,16 @@ for S in "$@"; do
         --master-port 29517 bench.py --dist --envs 131072 --steps 200 --warmup 20 --no-cpu-baseline \
         > $O/rccl.json 2> $O/rccl.err || { tail -30 $O/rccl.err; exit 1; }
       cat $O/rccl.json ;;
+    ranks)
+      # the sharded path rehearsed on one GPU: 2 and 4 ranks (gloo counters, every rank on GPU 0) at the full
+      # configs[4] batch; every rank's per-env output digests against the single-process run's
+      timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 --no-cpu-baseline --digest $O/dg1 > $O/ranks_1.json 2> $O/ranks_1.err || { tail -20 $O/ranks_1.err; exit 1; }
+      for N in 2 4; do
+        PGTG_BENCH_SAME_GPU=1 PGTG_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node $N --master-addr 127.0.0.1 --master-port $((29600 + N)) bench.py --gpus $N --steps 30 \
+          --warmup 10 --no-cpu-baseline --digest $O/dg$N > $O/ranks_$N.json 2> $O/ranks_$N.err || { tail -30 $O/ranks_$N.err; exit 1; }
+        python tools/digest_compare.py $O/dg1 $O/dg$N | tee $O/digest_compare_$N.json || exit 1
+      done ;;
     shards)
       for N in 1048576 524288 262144 131072; do
         timeout -k 10 300 python -u bench.py --envs $N --steps 400 --warmup 30 --no-cpu-baseline > $O/shard_$N.json 2> $O/shard_$N.err || { tail -20 $O/shard_$N.err; exit 1; }
