@@ -72,7 +72,8 @@ for S in "$@"; do
           --nproc-per-node $N --master-addr 127.0.0.1 --master-port $((29600 + N)) bench.py --gpus $N --steps 30 \
           --warmup 10 --no-cpu-baseline --digest $O/dg$N > $O/ranks_$N.json 2> $O/ranks_$N.err || { tail -30 $O/ranks_$N.err; exit 1; }
         python tools/digest_compare.py $O/dg1 $O/dg$N | tee $O/digest_compare_$N.json || exit 1
-      done ;;
+      done
+      rm -f $O/dg*.npz ;;  # (64 MB each: gpurun returns at most 64 MiB)
     shards)
       for N in 1048576 524288 262144 131072; do
         timeout -k 10 300 python -u bench.py --envs $N --steps 400 --warmup 30 --no-cpu-baseline > $O/shard_$N.json 2> $O/shard_$N.err || { tail -20 $O/shard_$N.err; exit 1; }
