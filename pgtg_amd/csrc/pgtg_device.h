@@ -194,9 +194,12 @@ struct DevState {
   uint32_t* tr_list;      // [n] envs k_env reset this launch (k_traffic's work list)
   uint32_t* tr_count;     // [2] list lengths, alternating launches
   // map queue (k_envq): per env a ring of kQueueDepth pre-generated episode maps, entry = plan
-  // words then {px | py<<16, sg, path_len | error<<16, 0}; qstate = count | head<<2 (0: empty)
+  // words then {px | py<<16, sg, path_len | error<<16, spawn tag}; qstate = head slot | kQueueStale
   uint32_t* qbuf;         // [n][kQueueDepth][qrec_dw] or null
   uint8_t* qstate;        // [n] or null
+  uint2* qreq;            // [2][grid][cap] refill requests {env << 1 | slot, spawn counter} per k_envq
+                          // workgroup, alternating launches
+  uint32_t* qctr;         // [2][kMaxQueueGrid] those lists' lengths, then [3] block counters (rotating)
   uint8_t* err;           // [n] last error code (negated PGTG_E_*)
   unsigned long long* counters;  // [2]: env steps, episodes
   unsigned long long* wg_ticks;  // [1]: wall-clock ticks of workgroup 0 in the last launch (start offsets)

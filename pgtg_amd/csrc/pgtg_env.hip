@@ -2733,17 +2733,25 @@ struct Lds {
   int img_in_traf;     // k_env with traffic: the whole workgroup's image in the (after the car pass dead)
                        // traffic region; the agent tile's counters and the reset hand-over words in hist
   int abl;             // diagnostic ablations (PGTG_TUNING builds only, PGTG_ABL; always 0 otherwise):
-                       // k_envq bit 0 no ring refills, bit 1 no terminal-observation writes, bit 2 no
-                       // observation writes, bit 3 the helper spins `spin` dependent VALU steps instead
-                       // of refilling, bit 4 refills without the ring-entry stores (timing experiments:
-                       // the results are wrong)
-  int spin;
+                       // k_envq bit 0 no ring refills (the stale entries taken as they are), bit 1 no
+                       // terminal-observation writes, bit 2 no observation writes, bit 4 refills without
+                       // the ring-entry stores (timing experiments: the results are wrong)
 };
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
+constexpr int kMaxQueueGrid = 4096;  // k_envq's persistent grid at most
+// refill requests one k_envq workgroup may make per launch (three times its share of the blocks: a
+// workgroup stops taking blocks before it could exceed them)
+__host__ __device__ inline uint64_t queue_req_cap(uint64_t nblk, uint64_t grid, int envs) {
+  return 3 * ((nblk + grid - 1) / grid) * (uint64_t)envs;
+}
 constexpr uint64_t kStaggerMaxTicks = 20000;  // 200 us of 100 MHz wall clock: a bound, never reached
-constexpr int kQueueDepth = 3;   // queued maps per env (a ring)
+constexpr int kQueueDepth = 2;   // queued maps per env (a ring: the next two episodes')
+constexpr uint32_t kQueueStale = 0x80u;  // qstate flag: the ring's entries are not this env's (k_qfill)
 constexpr int kViewDw = 8;       // k_envq with <= 32 envs: an env's view words for the image builders
 
+// a ring entry's spawn tag (its last word): the spawn counter it was generated for, inverted so that
+// zeroed memory matches none
+__host__ __device__ inline uint32_t queue_tag(uint32_t spawn) { return ~spawn; }
 __host__ __device__ inline int odd_up(int x) { return x | 1; }
 // words of a dense observation image of `envs` envs (+2: the writers' funnel reads run one word
 // ahead; a multiple of 4 so that what follows stays 16-byte aligned)
@@ -2772,10 +2780,8 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.stagger_wgs = 0;
   l.img_in_traf = 0;
   l.abl = 0;
-  l.spin = 0;
 #ifdef PGTG_TUNING  // A/B and diagnostic builds only: the product library reads no environment
   if (const char* e = getenv("PGTG_ABL")) l.abl = atoi(e);
-  if (const char* e = getenv("PGTG_SPIN")) l.spin = atoi(e);
   if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);
   if (const char* e = getenv("PGTG_COMPACT")) l.compact = atoi(e);
   if (const char* e = getenv("PGTG_QUEUE")) l.queue = l.queue && atoi(e);
@@ -2784,7 +2790,7 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   return l;
 }
 // After the observation image: sel[kBlock] | 32 B (k_env: per-wave reset ballots) or 128 B (k_envq:
-// refill masks, barrier counter) | the terminal-observation line mask (lm_words) | k_envq: the
+// barrier counter) | the terminal-observation line mask (lm_words) | k_envq: the
 // refill lanes' plan scratch (gen_off).  Recomputed whenever the image size changes.
 __host__ inline int tail_bytes(const Lds& l) {
   return kBlock + (l.queue ? 128 : 32) + 4 * l.lm_words + (l.queue && l.envs <= 32 ? 4 * kViewDw * l.envs : 0);
@@ -3156,7 +3162,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
                                (occ_valid && !reset_now ? kTrafOccValid : 0u) | (ts.fresh ? kTrafFresh : 0u));
     }
     if (mode != MODE_OBSERVE || err) S.err[i] = (uint8_t)(-err);
-    if (S.qstate && reset_now) S.qstate[i] = 0;  // maps generated here: the queued ones are stale
+    if (S.qstate && reset_now) S.qstate[i] = (uint8_t)kQueueStale;  // maps generated here: the queued ones are stale
   }
   if (TR && c.need_car) {
     // k_traffic's work list: one wave-aggregated atomic per wave
@@ -3246,10 +3252,10 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
   }
   d4[pwords / 4] = make_uint4(((uint32_t)px & 0xffffu) | ((uint32_t)py << 16),
                               (uint32_t)st_t | (uint32_t)st_d << 8 | (uint32_t)gl_t << 16 | (uint32_t)gl_d << 24,
-                              (uint32_t)len | (uint32_t)(-err) << 16, 0u);
+                              (uint32_t)len | (uint32_t)(-err) << 16, queue_tag(k));
 }
 
-// k_envq ablations (tools/ablate.sh): compiled in only in the tuning build; the product kernel tests
+// k_envq ablations (tools/ab_multi.sh, PGTG_ABL): compiled in only in the tuning build; the product kernel tests
 // no runtime flag for them
 #ifdef PGTG_TUNING
 #define ABLATE(L, bit) (((L).abl & (bit)) != 0)
@@ -3269,12 +3275,18 @@ __device__ __forceinline__ void sub_barrier(uint32_t* ctr, uint32_t target) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// Step launch with the map queue (no traffic; workgroups of <= 192 envs).  Wave `env_waves` (the
-// first without env slots) refills the rings of the envs that took a map in earlier launches --
-// at most kQueueLanes entries per launch, empty rings' heads first -- while the other waves step,
-// write the terminal observations, take queued maps for the envs that finished and write the new
-// observations, synchronising among themselves only.  Only when some env's ring is empty (the
-// first step after a reset, or a refill carried over) do they wait for the head refills.
+// Step launch with the map queue (no traffic; workgroups of <= 192 envs), persistent: the grid is the
+// workgroups resident at once; each takes env block blockIdx.x, then the next free one from a counter
+// (fetched one block ahead), until none is left.  Its env and writer waves step a block, write the
+// terminal observations, take the ring heads of the envs that finished -- requesting the
+// next-but-one episode's map for the slot taken, in the workgroup's own list -- and write the new
+// observations, synchronising among themselves only.  Its helper wave (wave `env_waves`, the first
+// without env slots) meanwhile generates the maps its workgroup requested in the previous launch,
+// kQueueLanes at a time, so that neither role waits for the other at a block's end.  A request made
+// in launch t is served in launch t + 1 and its entry taken in t + 2 at the earliest: two entries
+// per env suffice, and no entry is written while it can be read.
+// (One shared request list instead: 497 vs 456 us per 1 048 576-env launch, its counter a hot spot on
+// every env wave's path; static blocks blockIdx.x + k * gridDim.x: 455 us against the counter's 424.)
 // The map-queue step's observation images.  With <= 32 envs per workgroup they all sit in wave 0
 // and most of its lanes are idle, so each env's image is built by a group of G = 192 / E lanes of
 // the three non-helper waves (the env wave publishes its envs' views in LDS): lane e of wave 0 (the
@@ -3333,255 +3345,227 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
 template <bool BIG>
 __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
                                                     DevState S, const uint8_t* __restrict__ actions, PgtgOutputs out,
-                                                    Lds L) {
+                                                    Lds L, uint32_t qsel) {
   extern __shared__ uint32_t lds[];
   const DevCfg& c = *cfg;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint64_t t_start = stagger_start(L, S);
-  STAMP(0);
   stage_tables(gtab, false);  // (the map queue runs without lane channels: no sTX reference here)
-  const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
-  const int nb = (int)min((uint64_t)L.envs, S.n - env0);
   const int env_waves = (L.envs + 63) / 64, gen_wave = env_waves;
-  // ring entries of levels 1.. regenerated per launch: one per helper lane, two with three env waves
-  // (192 envs reset ~80 times per launch at configs[4]'s rate)
-  const int qcap = env_waves > 2 ? 2 * kQueueLanes : kQueueLanes;
   const bool env_wave = wave < env_waves;
-#if defined(PGTG_ENV_PRIO) && PGTG_ENV_PRIO > 0
-  // (A/B) the env and writer waves ahead of the map-generating wave in VALU arbitration
-  if (wave != gen_wave) __builtin_amdgcn_s_setprio(PGTG_ENV_PRIO);
-#endif
-  const int slot = tid;
-  const uint64_t i = env0 + slot;
-  const bool live = env_wave && slot < nb;
+  // refill requests: this launch's into list qsel & 3 (buffer qsel >> 2), the previous launch's from
+  // list (qsel + 2) % 3 (the other buffer); the third list's counters are cleared for the next launch
+  const uint32_t par = qsel >> 2;
+  const uint64_t nblk = (S.n + (uint64_t)L.envs - 1) / (uint64_t)L.envs;
+  const uint64_t cap = queue_req_cap(nblk, gridDim.x, L.envs);  // requests per workgroup and launch
+  uint2* req_new = S.qreq + ((uint64_t)par * gridDim.x + blockIdx.x) * cap;
+  const uint2* req_old = S.qreq + ((uint64_t)(par ^ 1u) * gridDim.x + blockIdx.x) * cap;
   const int pdw = L.plan_stride_dw;
-  uint32_t* plan_w = lds + (env_wave ? slot : 0) * pdw;
-  uint32_t* xf = lds + L.envs * pdw;  // per env slot: spawn counter, ring state at launch start
   uint32_t* st = lds + L.envs * (pdw + L.scratch_dw + L.traf_dw + L.hist_dw);
   uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
-  uint64_t* fm = reinterpret_cast<uint64_t*>(sel + kBlock);  // [level][env wave]: envs refilled at ring level
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(fm + 3 * kQueueDepth);  // sub_barrier counter
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(sel + kBlock);  // sub_barrier counter
   uint32_t* lm = L.lm_words ? reinterpret_cast<uint32_t*>(sel + kBlock + 128) : nullptr;  // terminal lines
   uint32_t* vw = reinterpret_cast<uint32_t*>(sel + kBlock + 128) + L.lm_words;  // env views (<= 32 envs)
-  Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
-
-  EnvView v{};
-  uint32_t qs = 0;
-  int act = 0;
-  if (live) {
-    v = rec_load(S.rec, i);
-    qs = S.qstate[i];
-    act = actions[i];  // issued with the staging loads, not on the step's chain
-    stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, pdw);
-    xf[slot * L.scratch_dw] = v.spawn;
-    xf[slot * L.scratch_dw + 1] = qs;
+  uint32_t* qn = ctr + 1;  // this launch's requests so far
+  uint32_t* nxt = ctr + 2;  // the next block
+  // blocks after the first: taken from a counter (three, rotating: this launch's, the next one's
+  // cleared here), one block ahead
+  uint32_t* bctr = S.qctr + 2 * kMaxQueueGrid;
+  if (blockIdx.x == 0 && tid == 0) bctr[((qsel & 3u) + 1u) % 3u] = 0u;
+  if (tid == 0) {
+    *ctr = 0u;
+    *qn = 0u;
   }
-  const uint32_t qn = qs & 3u, qh = (qs >> 2) & 3u;
-  if (env_wave) {  // refills: ring level l (0 = head) for the envs holding <= l maps
-#pragma unroll
-    for (int l = 0; l < kQueueDepth; l++) {
-      const uint64_t m = __ballot(live && qn <= (uint32_t)l);
-      if (lane == 0) fm[l * 3 + wave] = m;
-    }
-  }
-  if (tid == 0) *ctr = 0u;
-  for (int k = tid; k < L.lm_words; k += kBlock) lm[k] = 0u;
-  lds_barrier();  // tables, plans, refill masks, counter, line mask
-  STAMP(1);
-  // refills: the heads of empty rings (level 0, all of them), then levels 1.. in order (the first
-  // kQueueLanes this launch; the rest wait for a later launch)
-  int F[kQueueDepth];
-#pragma unroll
-  for (int l = 0; l < kQueueDepth; l++) {
-    F[l] = 0;
-    for (int w = 0; w < env_waves; w++) F[l] += __popcll(fm[l * 3 + w]);
-  }
-  const bool any_empty = F[0] != 0;
-#ifdef PGTG_STAMPS
-  if ((threadIdx.x & 63) == 0)  // diagnostic: empty rings and level-1/2 refills wanted in this workgroup
-    g_stamps[((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 32 + 12) & ((1 << 21) - 1)] =
-        (unsigned long long)F[0] | (unsigned long long)F[1] << 16 | (unsigned long long)F[2] << 32;
-#endif
+  lds_barrier();  // tables, counters
 
   if (wave == gen_wave) {
+    // the helper: the previous launch's requests, kQueueLanes at a time, until none is left
     uint16_t* gplan = reinterpret_cast<uint16_t*>(lds + L.gen_off + lane * pdw);
-    auto refill = [&](int k, int l) {
-      int e = 0, pre = 0;
-      for (int w = 0; w < env_waves; w++) {
-        const uint64_t m = fm[l * 3 + w];
-        const int cw = __popcll(m);
-        if (k >= pre && k < pre + cw) e = w * 64 + select64(m, k - pre);
-        pre += cw;
+    const uint32_t cnt = S.qctr[(par ^ 1u) * gridDim.x + blockIdx.x];
+    uint32_t made = 0;
+    if (!ABLATE(L, 1)) {
+      for (uint32_t base = 0; base < cnt; base += kQueueLanes) {
+        made += min((uint32_t)kQueueLanes, cnt - base);
+        if (base + (uint32_t)lane < cnt) {
+          const uint2 r = req_old[base + lane];
+          const uint64_t ie = r.x >> 1;
+          gen_queue_entry<BIG>(c, S, ie, r.y, gplan, pdw, S.qbuf + (ie * kQueueDepth + (r.x & 1u)) * (uint64_t)c.qrec_dw,
+                               ABLATE(L, 16));
+        }
       }
-      const uint64_t ie = env0 + e;
-      const uint32_t qe = xf[e * L.scratch_dw + 1];
-      const uint32_t rslot = (((qe >> 2) & 3u) + (uint32_t)l) % (uint32_t)kQueueDepth;
-      gen_queue_entry<BIG>(c, S, ie, xf[e * L.scratch_dw] + 5u * (uint32_t)l, gplan, pdw,
-                      S.qbuf + (ie * kQueueDepth + rslot) * (uint64_t)c.qrec_dw, ABLATE(L, 16));
-    };
-    if (ABLATE(L, 1)) {
-      if (any_empty) __syncthreads();
-      return;
     }
-#ifdef PGTG_TUNING
-    if (ABLATE(L, 8)) {  // issue without memory: a dependent VALU chain as long as a fill
-      uint32_t x = (uint32_t)tid;
-      for (int k = 0; k < L.spin; k++) x = x * 0x9e3779b1u + (x >> 7);
-      if (any_empty) __syncthreads();
-      if (x == 0x12345u) S.err[env0] = 9;
-      return;
-    }
-#endif
-    for (int k = lane; k < F[0]; k += kQueueLanes) refill(k, 0);  // every empty ring's head
-    if (any_empty) __syncthreads();  // head refills visible to the other waves
-    for (int k0 = lane; k0 < qcap; k0 += kQueueLanes) {  // levels 1.. in list order, up to qcap entries
-      int k = k0, l = 1;
-      while (l < kQueueDepth && k >= F[l]) {
-        k -= F[l];
-        l++;
-      }
-      if (l < kQueueDepth) refill(k, l);
-    }
-    if (lane == 0) {  // maps generated (S.counters[2]): the heads, then up to qcap for levels 1..
-      int rest = 0;
-      for (int l = 1; l < kQueueDepth; l++) rest += F[l];
-      atomicAdd(&S.counters[2], (unsigned long long)(F[0] + min(rest, qcap)));
-    }
+    if (lane == 0 && made) atomicAdd(&S.counters[2], (unsigned long long)made);  // maps generated
     STAMP(7);
     return;
   }
 
-  // ---- env and writer waves (all but the refill wave) ----
-  const int np = kBlock / 64 - 1;                            // participating waves
-  const int rank = (wave < gen_wave ? wave : wave - 1) * 64 + lane, nthr = np * 64;
+  // ---- env and writer waves (all but the helper), block after block ----
+  const int np = kBlock / 64 - 1;  // participating waves
+  const int nthr = np * 64;
   uint32_t bar = 0;  // running sub_barrier target
-  uint8_t my_sel = 0;
-  int err = 0;
-  if (live) {
-    StepResult res{0.0, 0.0, 0u};
-    bool occ_sat = false;
-    TrafState ts{0, 0, 0, 0};
-    err = env_step<false, BIG>(c, S, i, v, pl, act, res, nullptr, occ_sat, nullptr, ts, nullptr);
-    STAMP(22);
-    const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
-    if (out.reward) out.reward[i] = res.reward;
-    if (out.cost) out.cost[i] = res.cost;
-    if (out.terminated) out.terminated[i] = (v.flags & kFlagTerminated) ? 1 : 0;
-    if (out.truncated) out.truncated[i] = (v.flags & kFlagTruncated) ? 1 : 0;
-    if (out.braking) out.braking[i] = 0;
-    my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
-    if (BIG && res.plan_dirty && !my_sel) store_plan_row(c, S, i, plan_w, pdw);  // used subgoals (kPlanUsed)
-    if (lm && my_sel && out.final_obs) mark_lines(lm, out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)slot, (uint32_t)c.obs_bytes);
-    STAMP(23);
-  }
-  // the post-step image of every env (terminal for the finished ones)
-  {
-    ObsInfo oi;
-    group_obs<BIG>(c, S, v, live, st, oi, L, wave, lane, ctr, bar, np, rank, vw);
-    if (live) write_small_outputs(c, out, i, v, oi, my_sel == 1);
-  }
-  if (env_wave) sel[slot] = my_sel;
-  const uint64_t rm = __ballot(my_sel == 1);
-  if (env_wave && lane == 0 && rm) atomicAdd(&S.counters[1], (unsigned long long)__popcll(rm));
-  STAMP(2);
-  STAMP(28);
-  sub_barrier(ctr, bar += (uint32_t)np);
-  STAMP(29);
-  if (out.final_obs && !ABLATE(L, 2))
-    write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, rank, nthr, lm);
-  STAMP(3);
-  sub_barrier(ctr, bar += (uint32_t)np);  // terminal images written before they are rebuilt
-  if (any_empty) __syncthreads();  // the head refills
-  const bool reset_now = my_sel != 0;
-  if (reset_now) {  // the ring's head becomes the episode (env_reset without the generation)
-    const uint4* q4 = reinterpret_cast<const uint4*>(S.qbuf + (i * kQueueDepth + qh) * (uint64_t)c.qrec_dw);
-    uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
-    // all loads of the entry first: a load after a store to S.plan (which the compiler cannot
-    // tell apart from the queue) would wait for the one before it, one HBM latency per 16 bytes
-    const int nq = c.plan_stride / 8;  // 16-byte words of the tile plan (<= 8 unless BIG)
-    const uint4 meta = q4[nq];
-    for (int k0 = 0; k0 < (BIG ? nq : 1); k0 += 8) {
-      uint4 qw[8];
+  for (uint64_t blk = blockIdx.x; blk < nblk;) {
+    STAMP(0);
+    uint32_t got = 0xffffffffu;
+    if (tid == 0 && *qn + 2u * (uint32_t)L.envs <= cap) got = atomicAdd(&bctr[qsel & 3u], 1u);
+    // the per-lane values derive from an opaque copy of the lane id, block by block: hoisted out of
+    // the loop, they and what the compiler derives from them would hold registers through every
+    // block (the env waves spilled at 128 VGPRs)
+    int tid_o = tid;
+    asm volatile("" : "+v"(tid_o));
+    const int lane = tid_o & 63;
+    const int rank = (wave < gen_wave ? wave : wave - 1) * 64 + lane;
+    const int slot = tid_o;
+    uint32_t* plan_w = lds + (env_wave ? slot : 0) * pdw;
+    Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
+    const uint64_t env0 = blk * (uint64_t)L.envs;
+    const int nb = (int)min((uint64_t)L.envs, S.n - env0);
+    const uint64_t i = env0 + slot;
+    const bool live = env_wave && slot < nb;
+    EnvView v{};
+    uint32_t qh = 0;
+    int act = 0;
+    if (live) {
+      v = rec_load(S.rec, i);
+      qh = S.qstate[i] & 1u;
+      act = actions[i];  // issued with the staging loads, not on the step's chain
+      stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, pdw);
+    }
+    for (int k = rank; k < L.lm_words; k += nthr) lm[k] = 0u;
+    sub_barrier(ctr, bar += (uint32_t)np);  // plans, line mask (and the last block's images written)
+    STAMP(1);
+    uint8_t my_sel = 0;
+    int err = 0;
+    if (live) {
+      StepResult res{0.0, 0.0, 0u};
+      bool occ_sat = false;
+      TrafState ts{0, 0, 0, 0};
+      err = env_step<false, BIG>(c, S, i, v, pl, act, res, nullptr, occ_sat, nullptr, ts, nullptr);
+      STAMP(22);
+      const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
+      if (out.reward) out.reward[i] = res.reward;
+      if (out.cost) out.cost[i] = res.cost;
+      if (out.terminated) out.terminated[i] = (v.flags & kFlagTerminated) ? 1 : 0;
+      if (out.truncated) out.truncated[i] = (v.flags & kFlagTruncated) ? 1 : 0;
+      if (out.braking) out.braking[i] = 0;
+      my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
+      if (BIG && res.plan_dirty && !my_sel) store_plan_row(c, S, i, plan_w, pdw);  // used subgoals (kPlanUsed)
+      if (lm && my_sel && out.final_obs) mark_lines(lm, out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)slot, (uint32_t)c.obs_bytes);
+      STAMP(23);
+    }
+    // the post-step image of every env (terminal for the finished ones)
+    {
+      ObsInfo oi;
+      group_obs<BIG>(c, S, v, live, st, oi, L, wave, lane, ctr, bar, np, rank, vw);
+      if (live) write_small_outputs(c, out, i, v, oi, my_sel == 1);
+    }
+    if (env_wave) sel[slot] = my_sel;
+    const uint64_t rm = __ballot(my_sel == 1);
+    if (env_wave && lane == 0 && rm) atomicAdd(&S.counters[1], (unsigned long long)__popcll(rm));
+    STAMP(2);
+    STAMP(28);
+    sub_barrier(ctr, bar += (uint32_t)np);
+    STAMP(29);
+    if (out.final_obs && !ABLATE(L, 2))
+      write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, rank, nthr, lm);
+    STAMP(3);
+    sub_barrier(ctr, bar += (uint32_t)np);  // terminal images written before they are rebuilt
+    const bool reset_now = my_sel != 0;
+    const uint32_t k0 = v.spawn;
+    if (reset_now) {  // the ring's head becomes the episode (env_reset without the generation)
+      const uint4* q4 = reinterpret_cast<const uint4*>(S.qbuf + (i * kQueueDepth + qh) * (uint64_t)c.qrec_dw);
+      uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
+      // all loads of the entry first: a load after a store to S.plan (which the compiler cannot
+      // tell apart from the queue) would wait for the one before it, one HBM latency per 16 bytes
+      const int nq = c.plan_stride / 8;  // 16-byte words of the tile plan (<= 8 unless BIG)
+      const uint4 meta = q4[nq];
+      for (int k0q = 0; k0q < (BIG ? nq : 1); k0q += 8) {
+        uint4 qw[8];
 #pragma unroll
-      for (int k = 0; k < 8; k++) qw[k] = q4[k0 + k < nq ? k0 + k : k0];  // unconditional: registers, not scratch
+        for (int k = 0; k < 8; k++) qw[k] = q4[k0q + k < nq ? k0q + k : k0q];  // unconditional: registers, not scratch
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        if (k0 + k < nq) {
-          dstp[k0 + k] = qw[k];
-          const uint32_t wv[4] = {qw[k].x, qw[k].y, qw[k].z, qw[k].w};
+        for (int k = 0; k < 8; k++) {
+          if (k0q + k < nq) {
+            dstp[k0q + k] = qw[k];
+            const uint32_t wv[4] = {qw[k].x, qw[k].y, qw[k].z, qw[k].w};
 #pragma unroll
-          for (int j = 0; j < 4; j++)
-            if ((k0 + k) * 4 + j < pdw) plan_w[(k0 + k) * 4 + j] = wv[j];
+            for (int j = 0; j < 4; j++)
+              if ((k0q + k) * 4 + j < pdw) plan_w[(k0q + k) * 4 + j] = wv[j];
+          }
         }
       }
+      if (c.need_ice || c.need_broken || c.need_sand) {
+        SeedPool sp = ss_pool(S.seed[i]);
+        if (c.need_ice) stream_store_all(S.ice, i, ss_child(sp, k0 + 2u));
+        if (c.need_broken) stream_store_all(S.broken, i, ss_child(sp, k0 + 3u));
+        if (c.need_sand) stream_store_all(S.sand, i, ss_child(sp, k0 + 4u));
+      }
+      v.spawn = k0 + 5u;
+      v.sg = meta.y;
+      v.used = 0;
+      v.path_len = meta.z & 0xffffu;
+      v.flags = 0;
+      v.phase = 0;
+      v.elapsed = 0;
+      v.vx = v.vy = 0;
+      v.px = (int)(int16_t)(meta.x & 0xffffu);
+      v.py = (int)(int16_t)(meta.x >> 16);
+      // the entry was generated for this episode (spawn counter k0): every launch serves all of the
+      // previous launch's requests and the ring holds two entries, so it always is -- a mismatch is
+      // reported as a device error, never used
+      const int e2 = (meta.w != queue_tag(k0) && !ABLATE(L, 1)) ? PGTG_E_DEVICE : -(int)(meta.z >> 16);
+      if (e2) err = e2;
+      if (S.visited && e2 == 0) {
+        uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
+        for (int q2 = 0; q2 < c.vis_words; q2++) vis[q2] = 0;
+        int b = (v.px + 2) * c.vis_pitch + (v.py + 2);
+        vis[b >> 5] |= 1u << (b & 31);
+      }
     }
-    const uint32_t k0 = v.spawn;
-    if (c.need_ice || c.need_broken || c.need_sand) {
-      SeedPool sp = ss_pool(S.seed[i]);
-      if (c.need_ice) stream_store_all(S.ice, i, ss_child(sp, k0 + 2u));
-      if (c.need_broken) stream_store_all(S.broken, i, ss_child(sp, k0 + 3u));
-      if (c.need_sand) stream_store_all(S.sand, i, ss_child(sp, k0 + 4u));
+    STAMP(4);
+    // refill request: the next-but-one episode's map (spawn counter k0 + 10) into the slot just taken
+    const uint64_t rb = __ballot(reset_now);
+    if (rb) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(qn, (uint32_t)__popcll(rb));
+      base = __builtin_amdgcn_readfirstlane(base);
+      if (reset_now) {
+        req_new[base + __popcll(rb & ((1ull << lane) - 1ull))] = make_uint2((uint32_t)i << 1 | qh, k0 + 10u);
+        S.qstate[i] = (uint8_t)(qh ^ 1u);
+      }
     }
-    v.spawn = k0 + 5u;
-    v.sg = meta.y;
-    v.used = 0;
-    v.path_len = meta.z & 0xffffu;
-    v.flags = 0;
-    v.phase = 0;
-    v.elapsed = 0;
-    v.vx = v.vy = 0;
-    v.px = (int)(int16_t)(meta.x & 0xffffu);
-    v.py = (int)(int16_t)(meta.x >> 16);
-    const int e2 = -(int)(meta.z >> 16);
-    if (e2) err = e2;
-    if (S.visited && e2 == 0) {
-      uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
-      for (int q2 = 0; q2 < c.vis_words; q2++) vis[q2] = 0;
-      int b = (v.px + 2) * c.vis_pitch + (v.py + 2);
-      vis[b >> 5] |= 1u << (b & 31);
+    if (live) {
+      rec_store(S.rec, i, v);
+      S.err[i] = (uint8_t)(-err);
     }
+    STAMP(5);
+    {
+      ObsInfo oi;
+      group_obs<BIG>(c, S, v, reset_now, st, oi, L, wave, lane, ctr, bar, np, rank, vw, false);
+      if (reset_now) write_small_outputs(c, out, i, v, oi, false);
+    }
+    STAMP(30);
+    sub_barrier(ctr, bar += (uint32_t)np);
+    STAMP(31);
+    if (tid == 0) {
+      S.qctr[par * gridDim.x + blockIdx.x] = *qn;  // (every request of the block is in)
+      *nxt = got;
+    }
+    if (out.obs && !ABLATE(L, 4))
+      write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr, rank, nthr);
+    if (tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
+    if (blk == blockIdx.x) stagger_record(L, S, t_start);
+    STAMP(6);
+    const uint32_t g = *nxt;  // (written before the last barrier; rewritten only after the next one)
+    blk = g == 0xffffffffu ? nblk : (uint64_t)gridDim.x + g;
   }
-  STAMP(4);
-  if (live) {
-    rec_store(S.rec, i, v);
-    S.err[i] = (uint8_t)(-err);
-    // ring entries after this launch: the refills served (same list order as the refill wave)
-    // minus the head a reset took
-    uint32_t have = qn == 0u ? 1u : qn;
-    int base = 0;  // list index of the first item of the level
-#pragma unroll
-    for (int l = 1; l < kQueueDepth; l++) {
-      int pre = 0;
-      for (int w = 0; w < wave; w++) pre += __popcll(fm[l * 3 + w]);
-      if (qn <= (uint32_t)l && base + pre + __popcll(fm[l * 3 + wave] & ((1ull << lane) - 1ull)) < qcap) have++;
-      base += F[l];
-    }
-    const uint32_t nq = reset_now ? have - 1u : have;  // have >= 1: every head is refilled
-    const uint32_t nh = reset_now ? (qh + 1u) % (uint32_t)kQueueDepth : qh;
-    S.qstate[i] = (uint8_t)(nq | nh << 2);
-  }
-  STAMP(5);
-  {
-    ObsInfo oi;
-    group_obs<BIG>(c, S, v, reset_now, st, oi, L, wave, lane, ctr, bar, np, rank, vw, false);
-    if (reset_now) write_small_outputs(c, out, i, v, oi, false);
-  }
-  STAMP(30);
-  sub_barrier(ctr, bar += (uint32_t)np);
-  STAMP(31);
-  if (out.obs && !ABLATE(L, 4))
-    write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr, rank, nthr);
-  if (tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
-  stagger_record(L, S, t_start);
-  STAMP(6);
 }
 
-// Fill every env's map ring (after a reset, whose k_env launch generated the current episodes' maps and
-// emptied the rings): one lane per env generates the missing entries in ring order, spawn counters
-// spawn, spawn + 5, spawn + 10 -- the maps k_envq's helper wave would generate over the first launches
-// (while the env waves wait for the heads), so that the first step launches run in the steady state the
-// rings keep from then on.  The entries are a function of (seed, spawn counter) alone: results are
-// unchanged.
+// Fill every env's map ring: after a reset launch (whose k_env generated the current episodes' maps
+// and marked the reset envs' rings stale), a state dump (the requests still pending) or a change of
+// step kernel.  One lane per env checks both entries' spawn tags against the env's next two episodes
+// (spawn counters s and s + 5, the head first) and generates the ones that do not match -- the maps
+// k_envq's helpers would generate -- so that the step launches start with full rings.  The entries
+// are a function of (seed, spawn counter) alone: results are unchanged.
 template <bool BIG>
 __global__ void __launch_bounds__(kBlock) k_qfill(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
                                                   DevState S, int pdw) {
@@ -3592,16 +3576,20 @@ __global__ void __launch_bounds__(kBlock) k_qfill(const DevCfg* __restrict__ cfg
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   uint32_t made = 0;
   if (i < S.n) {
-    const uint32_t qs = S.qstate[i], qn = qs & 3u, qh = (qs >> 2) & 3u;
-    if (qn < (uint32_t)kQueueDepth) {
-      const uint32_t spawn = S.rec[i].b.y;  // EnvRec w5
-      uint16_t* plan = reinterpret_cast<uint16_t*>(lds + threadIdx.x * pdw);
-      for (uint32_t l = qn; l < (uint32_t)kQueueDepth; l++)
-        gen_queue_entry<BIG>(c, S, i, spawn + 5u * l, plan, pdw,
-                             S.qbuf + (i * kQueueDepth + (qh + l) % (uint32_t)kQueueDepth) * (uint64_t)c.qrec_dw);
-      S.qstate[i] = (uint8_t)(kQueueDepth | qh << 2);
-      made = (uint32_t)kQueueDepth - qn;
+    const uint32_t qs = S.qstate[i];
+    const bool stale = (qs & kQueueStale) != 0;
+    const uint32_t qh = stale ? 0u : (qs & 1u);
+    const uint32_t spawn = S.rec[i].b.y;  // EnvRec w5
+    const int tag_w = (c.plan_stride / 8) * 4 + 3;
+    uint16_t* plan = reinterpret_cast<uint16_t*>(lds + threadIdx.x * pdw);
+    for (uint32_t l = 0; l < (uint32_t)kQueueDepth; l++) {
+      uint32_t* dst = S.qbuf + (i * kQueueDepth + (qh ^ l)) * (uint64_t)c.qrec_dw;
+      if (stale || dst[tag_w] != queue_tag(spawn + 5u * l)) {
+        gen_queue_entry<BIG>(c, S, i, spawn + 5u * l, plan, pdw, dst);
+        made++;
+      }
     }
+    if (stale) S.qstate[i] = 0;
   }
   // maps generated (S.counters[2]): one atomic per wave
   const uint32_t wsum = (uint32_t)__popcll(__ballot(made & 1u)) + 2u * (uint32_t)__popcll(__ballot(made & 2u));
@@ -3884,6 +3872,9 @@ struct pgtg_handle {
   int kt_grid = 0, kt_cap = 16;
   int kt_plan_dw = 0, kt_rs_dw = 0;
   size_t kt_lds = 0;
+  // k_envq: step launches so far (its request lists rotate per launch) and its persistent grid
+  uint64_t q_launch = 0;
+  uint64_t q_grid = 0;
 };
 
 
@@ -4379,6 +4370,10 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
     // one round: 66 -> 78 us, profiles/r03/abrec/stagger_by_shard.txt)
     const uint64_t blocks = (h->n + h->L.envs - 1) / h->L.envs;
     h->L.stagger = blocks >= (uint64_t)2 * h->L.stagger_wgs ? 1 : 0;
+    // k_envq: the workgroups resident at once
+    // (more, with the later ones waiting for a slot: 125 % of them 429 vs 424 us per 1 048 576-env
+    // launch, 150 % 450 us)
+    h->q_grid = std::max<uint64_t>(1, std::min(std::min(blocks, (uint64_t)h->L.stagger_wgs), (uint64_t)kMaxQueueGrid));
 #ifdef PGTG_TUNING
     if (const char* e = getenv("PGTG_STAGGER")) h->L.stagger = atoi(e);
 #endif
@@ -4539,7 +4534,9 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     return rc;
   }
   if (h->L.queue) {
-    if ((rc = dalloc(h, &h->S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw)) || (rc = dalloc(h, &h->S.qstate, n))) {
+    if ((rc = dalloc(h, &h->S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw)) || (rc = dalloc(h, &h->S.qstate, n)) ||
+        (rc = dalloc(h, &h->S.qreq, 2 * h->q_grid * queue_req_cap((n + h->L.envs - 1) / h->L.envs, h->q_grid, h->L.envs))) ||
+        (rc = dalloc(h, &h->S.qctr, 2 * kMaxQueueGrid + 3))) {
       g_create_err = h->err;
       pgtg_destroy(h);
       return rc;
@@ -4587,8 +4584,10 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
   const void* fn = step_fn(h, mode);
   void* args[] = {&h->dcfg, &h->dtab, &h->S, &actions, &mask, &h->out, &mode, &h->L, &h->tr_slot};
   if (fn == (const void*)k_envq<false> || fn == (const void*)k_envq<true>) {
-    void* qargs[] = {&h->dcfg, &h->dtab, &h->S, &actions, &h->out, &h->L};
-    HIPCHK(h, hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(kBlock), qargs, h->lds, h->stream));
+    uint32_t qsel = (uint32_t)(h->q_launch % 3) | (uint32_t)(h->q_launch & 1) << 2;
+    h->q_launch++;
+    void* qargs[] = {&h->dcfg, &h->dtab, &h->S, &actions, &h->out, &h->L, &qsel};
+    HIPCHK(h, hipLaunchKernel(fn, dim3((unsigned)std::min(blocks, h->q_grid)), dim3(kBlock), qargs, h->lds, h->stream));
   } else {
     HIPCHK(h, hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(kBlock), args, h->lds, h->stream));
   }
@@ -4608,9 +4607,12 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
   return PGTG_OK;
 }
 
-// After a reset launch of a map-queue handle: fill the rings the reset emptied (k_qfill).
+// After a reset launch of a map-queue handle, before a state dump and when the step kernel changes:
+// drop the pending refill requests and fill every ring (k_qfill) -- the entries the requests asked for
+// and the rings of the envs a reset gave new maps.
 static int queue_fill(pgtg_handle* h) {
   if (!h->L.queue || !h->S.qbuf) return PGTG_OK;
+  HIPCHK(h, hipMemsetAsync(h->S.qctr, 0, (2 * kMaxQueueGrid + 3) * sizeof(uint32_t), h->stream));
 #ifdef PGTG_TUNING
   if (const char* e = getenv("PGTG_QFILL"))
     if (!atoi(e)) return PGTG_OK;
@@ -4861,10 +4863,12 @@ int pgtg_set_rules(pgtg_handle* h, const PgtgRule* rules, int32_t n_rules) {
       return rc;
     }
   }
+  const bool refill = h->L.queue && !old_L.queue;  // back to k_envq: rings k_env's resets left stale
   uint8_t w[PGTG_MAX_RULES][6][20] = {};
   for (int k = 0; k < n_rules; k++) memcpy(w[k], rules[k].weight, sizeof w[k]);
   HIPCHK(h, hipMemcpy(h->dcfg, &c, sizeof(DevCfg), hipMemcpyHostToDevice));
   HIPCHK(h, hipMemcpy(reinterpret_cast<uint8_t*>(h->dtab) + kTabHead + offsetof(TablesTail, rule_w), w, sizeof w, hipMemcpyHostToDevice));
+  if (refill) return queue_fill(h);
   return PGTG_OK;
 }
 
@@ -4921,7 +4925,7 @@ struct PgtgSectionEntry {
   uint32_t id, pad;
   uint64_t bytes;
 };
-constexpr uint32_t kStateVersion = 4;
+constexpr uint32_t kStateVersion = 5;
 uint64_t cfg_hash(const DevCfg& c) {  // DevCfg is zero-initialised (derive_cfg), so padding hashes as 0
   const uint8_t* p = reinterpret_cast<const uint8_t*>(&c);
   uint64_t h = 0xcbf29ce484222325ull;
@@ -4981,6 +4985,9 @@ int pgtg_dump_state(pgtg_handle* h, void* buf, uint64_t bytes) {
   const auto v = state_sections(h);
   if (bytes < state_blob_bytes(v)) return fail(h, PGTG_E_INVALID, "pgtg_dump_state: buffer smaller than pgtg_state_size");
   HIPCHK(h, hipSetDevice(h->device));
+  // the map rings complete (the pending refill requests served now rather than by the next step
+  // launch): the blob holds no request list, whose order depends on timing
+  if (int rc = queue_fill(h)) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   uint8_t* p = static_cast<uint8_t*>(buf);
   PgtgStateHeader hd{};
@@ -5043,6 +5050,7 @@ int pgtg_load_state(pgtg_handle* h, const void* buf, uint64_t bytes) {
     off += s.bytes;
   }
   if (h->S.tr_count) HIPCHK(h, hipMemset(h->S.tr_count, 0, 2 * sizeof(uint32_t)));
+  if (h->S.qctr) HIPCHK(h, hipMemset(h->S.qctr, 0, (2 * kMaxQueueGrid + 3) * sizeof(uint32_t)));  // (dumped with full rings)
   return PGTG_OK;
 }
 

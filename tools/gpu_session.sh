@@ -14,6 +14,7 @@
 #   ranks            2 and 4 ranks on one GPU (gloo) at the full configs[4] batch, per-env digests vs one process
 #   shards           single-process lines at the per-rank shards of N = 2, 4, 8 (524 288 / 262 144 /
 #                    131 072 envs) beside the 1 048 576-env line
+#   adapter          bench.py --adapter device / host / host-monitor (the SB3 VecEnv adapter, caller workload)
 #   profile:<wl,..>  tools/gpu_profile.sh (rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes)
 #   genbench         map-generation latency per map (tools/genbench.py, stamps build)
 #   stamps:<wl,..>   per-phase cycle stamps (PGTG_STAMPS build, tools/stamps.py)
@@ -78,6 +79,11 @@ for S in "$@"; do
       for N in 1048576 524288 262144 131072; do
         timeout -k 10 300 python -u bench.py --envs $N --steps 400 --warmup 30 --no-cpu-baseline > $O/shard_$N.json 2> $O/shard_$N.err || { tail -20 $O/shard_$N.err; exit 1; }
         python tools/bench_line.py $O/shard_$N.json
+      done ;;
+    adapter)
+      for M in device host host-monitor; do
+        timeout -k 10 300 python -u bench.py --adapter $M --steps 200 --warmup 20 > $O/adapter_$M.json 2> $O/adapter_$M.err || { tail -20 $O/adapter_$M.err; exit 1; }
+        python -c "import json; d=json.load(open('$O/adapter_$M.json')); print('$M', round(d['value'] / 1e6, 2), 'M env-steps/s', round(d['ms_per_step'], 2), 'ms/step')"
       done ;;
     profile:*)
       R=${S#profile:}; timeout -k 10 1500 bash tools/gpu_profile.sh $TAG ${R//,/ } > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }

@@ -57,6 +57,7 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
     spread = kw.get("traffic_density", 0) > 0
     active = np.ones(nw, bool) if spread else (np.arange(nw) % 4) * 64 < E
     helper = (np.arange(nw) % 4) * 64 == ((E + 63) // 64) * 64
+    active &= st[:, 0] != 0  # (the persistent k_envq: only its grid's workgroups hold stamps)
     sh = st[helper]
     okh = (sh[:, 7] > sh[:, 0]) & (sh[:, 7] - sh[:, 0] < 1e8)
     if okh.any():  # map-queue helper wave (k_envq)
