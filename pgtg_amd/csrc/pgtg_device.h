@@ -94,9 +94,11 @@ struct DevCfg {
   int32_t nsd_off, nsd_pitch;   // nsd table index (dx+off)*pitch + (dy+off)
   int32_t cmp_off, cmp_pitch;   // compass table index
   int32_t vis_pitch, vis_words; // visited bitset: ((x+2)*vis_pitch + (y+2))
-  int32_t plan_stride;          // u16 per env in the global tile-plan array (multiple of 8)
+  int32_t plan_stride;          // u16 per env in the global tile-plan array (a multiple of 8; of 64, whole
+                                // lines, for the map queue's maps)
+  int32_t plan_dq;              // 16-byte quads of it that hold tiles ((nt + 7) / 8)
   int32_t obs_bytes;            // n_channels * win * win
-  int32_t qrec_dw;              // map-queue entry words (plan_stride / 2 + 4)
+  int32_t qrec_dw;              // map-queue entry words (plan_dq * 4 + 4, in whole 128-byte lines)
   int32_t mask_words;           // ceil(win*win/32)
   // per-tile arrays of maps up to 256 tiles, kept behind the fields every launch reads
   uint16_t fixed_plan[kMaxTiles];

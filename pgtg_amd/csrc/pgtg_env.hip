@@ -72,14 +72,13 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// One env's tile plan (plan_stride u16 words in HBM, a multiple of 8) into its LDS row of pdw words,
+// One env's tile plan (its nq data quads of 8 u16 in HBM) into its LDS row of pdw words,
 // in blocks of 8 x 16 bytes (BIG: maps of > 64 tiles; smaller maps are one block, straight-line code:
 // a runtime block loop made the compiler wait for every load before the first LDS store), each
 // block's loads first.
 template <bool BIG>
-__device__ __forceinline__ void stage_plan(const uint16_t* __restrict__ plan, int plan_stride, uint32_t* dst, int pdw) {
+__device__ __forceinline__ void stage_plan(const uint16_t* __restrict__ plan, int nq, uint32_t* dst, int pdw) {
   const uint4* src = reinterpret_cast<const uint4*>(plan);
-  const int nq = plan_stride / 8;
   for (int k0 = 0; k0 < (BIG ? nq : 1); k0 += 8) {
     uint4 q[8];
 #pragma unroll
@@ -2735,7 +2734,8 @@ struct Lds {
   int abl;             // diagnostic ablations (PGTG_TUNING builds only, PGTG_ABL; always 0 otherwise):
                        // k_envq bit 0 no ring refills (the stale entries taken as they are), bit 1 no
                        // terminal-observation writes, bit 2 no observation writes, bit 4 refills without
-                       // the ring-entry stores (timing experiments: the results are wrong)
+                       // the ring-entry stores, bit 5 no plan-row stores at resets (timing experiments:
+                       // the results are wrong)
 };
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
 constexpr int kMaxQueueGrid = 4096;  // k_envq's persistent grid at most
@@ -2946,7 +2946,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
       ts.fresh = (tr4.w & kTrafFresh) ? 1u : 0u;
       occ_valid = (tr4.w & kTrafOccValid) != 0u;
     }
-    stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, L.plan_stride_dw);
+    stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_dq, plan_w, L.plan_stride_dw);
   }
   for (int k = tid; k < L.lm_words; k += kBlock) lm[k] = 0u;
   lds_barrier();  // sT ready
@@ -3233,7 +3233,7 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
   }
   const uint32_t* pw = reinterpret_cast<const uint32_t*>(plan);
   uint4* d4 = reinterpret_cast<uint4*>(dst);
-  const int pwords = c.plan_stride / 2;
+  const int pwords = c.plan_dq * 4;
 #ifdef PGTG_TUNING
   if (no_store) {  // (timing experiment: the entry is built but not written)
     if (len == 12345 && px == 7) d4[0] = make_uint4(0, 0, 0, 0);
@@ -3253,6 +3253,7 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
   d4[pwords / 4] = make_uint4(((uint32_t)px & 0xffffu) | ((uint32_t)py << 16),
                               (uint32_t)st_t | (uint32_t)st_d << 8 | (uint32_t)gl_t << 16 | (uint32_t)gl_d << 24,
                               (uint32_t)len | (uint32_t)(-err) << 16, queue_tag(k));
+  for (int q = pwords / 4 + 1; q < c.qrec_dw / 4; q++) d4[q] = make_uint4(0u, 0u, 0u, 0u);  // the line's rest
 }
 
 // k_envq ablations (tools/ab_multi.sh, PGTG_ABL): compiled in only in the tuning build; the product kernel tests
@@ -3428,7 +3429,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       v = rec_load(S.rec, i);
       qh = S.qstate[i] & 1u;
       act = actions[i];  // issued with the staging loads, not on the step's chain
-      stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, pdw);
+      stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_dq, plan_w, pdw);
     }
     for (int k = rank; k < L.lm_words; k += nthr) lm[k] = 0u;
     sub_barrier(ctr, bar += (uint32_t)np);  // plans, line mask (and the last block's images written)
@@ -3476,7 +3477,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
       // all loads of the entry first: a load after a store to S.plan (which the compiler cannot
       // tell apart from the queue) would wait for the one before it, one HBM latency per 16 bytes
-      const int nq = c.plan_stride / 8;  // 16-byte words of the tile plan (<= 8 unless BIG)
+      const int nq = c.plan_dq;  // 16-byte words of the tile plan (<= 8 unless BIG)
       const uint4 meta = q4[nq];
       for (int k0q = 0; k0q < (BIG ? nq : 1); k0q += 8) {
         uint4 qw[8];
@@ -3485,7 +3486,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           if (k0q + k < nq) {
-            dstp[k0q + k] = qw[k];
+            if (!ABLATE(L, 32)) dstp[k0q + k] = qw[k];
             const uint32_t wv[4] = {qw[k].x, qw[k].y, qw[k].z, qw[k].w};
 #pragma unroll
             for (int j = 0; j < 4; j++)
@@ -3493,6 +3494,8 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
           }
         }
       }
+      if (!ABLATE(L, 32))
+        for (int k = nq; k < c.plan_stride / 8; k++) dstp[k] = make_uint4(0u, 0u, 0u, 0u);  // the row's whole lines
       if (c.need_ice || c.need_broken || c.need_sand) {
         SeedPool sp = ss_pool(S.seed[i]);
         if (c.need_ice) stream_store_all(S.ice, i, ss_child(sp, k0 + 2u));
@@ -3512,7 +3515,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       // the entry was generated for this episode (spawn counter k0): every launch serves all of the
       // previous launch's requests and the ring holds two entries, so it always is -- a mismatch is
       // reported as a device error, never used
-      const int e2 = (meta.w != queue_tag(k0) && !ABLATE(L, 1)) ? PGTG_E_DEVICE : -(int)(meta.z >> 16);
+      const int e2 = (meta.w != queue_tag(k0) && !ABLATE(L, 1 | 16)) ? PGTG_E_DEVICE : -(int)(meta.z >> 16);
       if (e2) err = e2;
       if (S.visited && e2 == 0) {
         uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
@@ -3530,7 +3533,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       base = __builtin_amdgcn_readfirstlane(base);
       if (reset_now) {
         req_new[base + __popcll(rb & ((1ull << lane) - 1ull))] = make_uint2((uint32_t)i << 1 | qh, k0 + 10u);
-        S.qstate[i] = (uint8_t)(qh ^ 1u);
+        S.qstate[i] = (uint8_t)(qh ^ 1u);  // (every env's byte instead: 403.3 vs 401.4 us)
       }
     }
     if (live) {
@@ -3580,7 +3583,7 @@ __global__ void __launch_bounds__(kBlock) k_qfill(const DevCfg* __restrict__ cfg
     const bool stale = (qs & kQueueStale) != 0;
     const uint32_t qh = stale ? 0u : (qs & 1u);
     const uint32_t spawn = S.rec[i].b.y;  // EnvRec w5
-    const int tag_w = (c.plan_stride / 8) * 4 + 3;
+    const int tag_w = c.plan_dq * 4 + 3;
     uint16_t* plan = reinterpret_cast<uint16_t*>(lds + threadIdx.x * pdw);
     for (uint32_t l = 0; l < (uint32_t)kQueueDepth; l++) {
       uint32_t* dst = S.qbuf + (i * kQueueDepth + (qh ^ l)) * (uint64_t)c.qrec_dw;
@@ -3677,8 +3680,8 @@ __global__ void __launch_bounds__(kBlock) k_traffic(const DevCfg* __restrict__ c
     const uint32_t j = (r * W + blockIdx.x * (kBlock / 64) + (uint32_t)wave) * e + (uint32_t)slot;
     if (j >= n) break;
     const uint64_t i = S.tr_list[j];
-    if (c.nt > kSmallTiles) stage_plan<true>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, plan_dw);
-    else stage_plan<false>(S.plan + i * (uint64_t)c.plan_stride, c.plan_stride, plan_w, plan_dw);
+    if (c.nt > kSmallTiles) stage_plan<true>(S.plan + i * (uint64_t)c.plan_stride, c.plan_dq, plan_w, plan_dw);
+    else stage_plan<false>(S.plan + i * (uint64_t)c.plan_stride, c.plan_dq, plan_w, plan_dw);
     Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
     const EnvView v = rec_load(S.rec, i);
     const int pix = min(max(0, v.px), c.W - 1), piy = min(max(0, v.py), c.H - 1);
@@ -4242,8 +4245,15 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
   c.cmp_pitch = 2 * c.cmp_off + 1;
   c.vis_pitch = c.H + 4;
   c.vis_words = ((c.W + 4) * (c.H + 4) + 31) / 32;
-  c.plan_stride = ((c.nt + 7) / 8) * 8;
-  c.qrec_dw = c.plan_stride / 2 + 4;
+  // plan rows, read as the quads that hold tiles.  Random maps of >= 16 tiles without traffic (the
+  // map queue's, whose resets copy rows): whole 128-byte lines, written whole (1 048 576 5x5 envs
+  // 401 -> 397 us per launch); smaller ones in 16-byte quads (262 144 3x3 envs: 128-byte rows 97
+  // against 92 us, the in-place resets writing four times the bytes)
+  c.plan_dq = (c.nt + 7) / 8;
+  c.plan_stride = (!c.need_car && !c.fixed_map && c.nt >= 16) ? ((c.nt + 63) / 64) * 64 : c.plan_dq * 8;
+  // map-queue entries in whole 128-byte lines, written whole: partly written lines cost the step
+  // launch 37 us of its 425 (1 048 576 5x5 envs, 80-byte entries)
+  c.qrec_dw = (c.plan_dq * 4 + 4 + 31) & ~31;
   return 0;
 }
 
