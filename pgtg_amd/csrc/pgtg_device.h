@@ -201,7 +201,8 @@ struct DevState {
   uint8_t* qstate;        // [n] or null
   uint2* qreq;            // [2][grid][cap] refill requests {env << 1 | slot, spawn counter} per k_envq
                           // workgroup, alternating launches
-  uint32_t* qctr;         // [2][kMaxQueueGrid] those lists' lengths, then [3] block counters (rotating)
+  uint2* qovf;            // [2][8][cap] one-round launches: the requests beyond a workgroup's first 64
+  uint32_t* qctr;         // the lists' lengths, block counters, overflow lengths and heads (kQctr*)
   uint8_t* err;           // [n] last error code (negated PGTG_E_*)
   unsigned long long* counters;  // [2]: env steps, episodes
   unsigned long long* wg_ticks;  // [1]: wall-clock ticks of workgroup 0 in the last launch (start offsets)

@@ -2739,10 +2739,22 @@ struct Lds {
 };
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
 constexpr int kMaxQueueGrid = 4096;  // k_envq's persistent grid at most
+// DevState::qctr: [2][kMaxQueueGrid] per-workgroup request counts (launch parity), [3] block
+// counters, then per rotating set (3) and overflow list (8, one per workgroup residue mod 8) the
+// overflow lists' lengths
+constexpr int kQctrBlocks = 2 * kMaxQueueGrid;
+constexpr int kQctrOvfLen = kQctrBlocks + 3;
+constexpr int kQctrWords = kQctrOvfLen + 24;
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o);
+  return x;
+}
 // refill requests one k_envq workgroup may make per launch (three times its share of the blocks: a
 // workgroup stops taking blocks before it could exceed them)
 __host__ __device__ inline uint64_t queue_req_cap(uint64_t nblk, uint64_t grid, int envs) {
-  return 3 * ((nblk + grid - 1) / grid) * (uint64_t)envs;
+  const uint64_t c = 3 * ((nblk + grid - 1) / grid) * (uint64_t)envs;
+  return c < (uint64_t)kQueueLanes ? (uint64_t)kQueueLanes : c;  // (the helper reads its first kQueueLanes ahead)
 }
 constexpr uint64_t kStaggerMaxTicks = 20000;  // 200 us of 100 MHz wall clock: a bound, never reached
 constexpr int kQueueDepth = 2;   // queued maps per env (a ring: the next two episodes')
@@ -3351,7 +3363,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   const DevCfg& c = *cfg;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint64_t t_start = stagger_start(L, S);
-  stage_tables(gtab, false);  // (the map queue runs without lane channels: no sTX reference here)
+  STAMP(0);  // (the env waves' is each block's start)
   const int env_waves = (L.envs + 63) / 64, gen_wave = env_waves;
   const bool env_wave = wave < env_waves;
   // refill requests: this launch's into list qsel & 3 (buffer qsel >> 2), the previous launch's from
@@ -3361,7 +3373,22 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   const uint64_t cap = queue_req_cap(nblk, gridDim.x, L.envs);  // requests per workgroup and launch
   uint2* req_new = S.qreq + ((uint64_t)par * gridDim.x + blockIdx.x) * cap;
   const uint2* req_old = S.qreq + ((uint64_t)(par ^ 1u) * gridDim.x + blockIdx.x) * cap;
+  // One round of blocks (every workgroup one block): a helper's time is on the launch's path, so a
+  // workgroup lists at most kQueueLanes requests (one batch) and appends the rest to an overflow
+  // list shared by the workgroups of its residue mod 8, whose helpers fill their spare lanes from it.
+  const bool one_round = nblk <= gridDim.x;
+  const uint32_t ox = blockIdx.x & 7u, set_new = qsel & 3u, set_old = (set_new + 2u) % 3u;
+  const uint64_t ocap = ((gridDim.x + 7u) / 8u) * (uint64_t)L.envs;  // an overflow list's capacity
+  // the helper's list length and first requests, issued before the tables are staged
+  uint32_t cnt = 0;
+  uint2 r0 = make_uint2(0u, 0u);
+  if (wave == gen_wave) {
+    cnt = S.qctr[(par ^ 1u) * gridDim.x + blockIdx.x];
+    r0 = req_old[lane];  // (cap >= kQueueLanes: inside the list, used only below cnt)
+  }
+  if (blockIdx.x == 0 && tid < 8) S.qctr[kQctrOvfLen + ((set_new + 1u) % 3u) * 8u + tid] = 0u;  // (the launch after next's)
   const int pdw = L.plan_stride_dw;
+  stage_tables(gtab, false);  // (the map queue runs without lane channels: no sTX reference here)
   uint32_t* st = lds + L.envs * (pdw + L.scratch_dw + L.traf_dw + L.hist_dw);
   uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
   uint32_t* ctr = reinterpret_cast<uint32_t*>(sel + kBlock);  // sub_barrier counter
@@ -3371,7 +3398,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   uint32_t* nxt = ctr + 2;  // the next block
   // blocks after the first: taken from a counter (three, rotating: this launch's, the next one's
   // cleared here), one block ahead
-  uint32_t* bctr = S.qctr + 2 * kMaxQueueGrid;
+  uint32_t* bctr = S.qctr + kQctrBlocks;
   if (blockIdx.x == 0 && tid == 0) bctr[((qsel & 3u) + 1u) % 3u] = 0u;
   if (tid == 0) {
     *ctr = 0u;
@@ -3380,15 +3407,50 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   lds_barrier();  // tables, counters
 
   if (wave == gen_wave) {
+    STAMP(1);
     // the helper: the previous launch's requests, kQueueLanes at a time, until none is left
     uint16_t* gplan = reinterpret_cast<uint16_t*>(lds + L.gen_off + lane * pdw);
-    const uint32_t cnt = S.qctr[(par ^ 1u) * gridDim.x + blockIdx.x];
     uint32_t made = 0;
     if (!ABLATE(L, 1)) {
-      for (uint32_t base = 0; base < cnt; base += kQueueLanes) {
-        made += min((uint32_t)kQueueLanes, cnt - base);
-        if (base + (uint32_t)lane < cnt) {
-          const uint2 r = req_old[base + lane];
+      // one round: this helper's share of its residue's overflow list -- as many as its spare lanes,
+      // after those of the workgroups before it (a prefix sum over their list lengths, no atomics:
+      // 128 helpers claiming from one counter waited 7 us for it); what outgrows every spare lane
+      // follows in whole batches by workgroup order
+      const uint2* ovf = S.qovf + ((uint64_t)(par ^ 1u) * 8u + ox) * ocap;
+      uint32_t ob = 0, on = 0, olen = 0, tot = 0;
+      const uint32_t nj = (gridDim.x - ox + 7u) / 8u, jme = blockIdx.x / 8u;
+      if (one_round) {
+        olen = S.qctr[kQctrOvfLen + set_old * 8u + ox];
+        if (olen > 0) {
+          uint32_t pre = 0;
+          for (uint32_t j0 = 0; j0 < nj; j0 += kQueueLanes) {
+            const uint32_t j = j0 + (uint32_t)lane;
+            const uint32_t sp = j < nj ? kQueueLanes - min(S.qctr[(par ^ 1u) * gridDim.x + ox + 8u * j], (uint32_t)kQueueLanes) : 0u;
+            pre += wave_sum(j < jme ? sp : 0u);
+            tot += wave_sum(sp);
+          }
+          on = olen > pre ? min(olen - pre, kQueueLanes - min(cnt, (uint32_t)kQueueLanes)) : 0u;
+          ob = pre;
+        }
+      }
+      for (uint32_t base = 0;; base += kQueueLanes) {  // the workgroup's own requests (and the spare lanes')
+        const uint32_t own = base < cnt ? min((uint32_t)kQueueLanes, cnt - base) : 0u;
+        const uint32_t oth = base == 0 ? on : 0u;
+        if (own + oth == 0) break;
+        made += own + oth;
+        if ((uint32_t)lane < own + oth) {
+          const uint2 r = (uint32_t)lane >= own ? ovf[ob + (lane - own)] : base == 0 ? r0 : req_old[base + lane];
+          const uint64_t ie = r.x >> 1;
+          gen_queue_entry<BIG>(c, S, ie, r.y, gplan, pdw, S.qbuf + (ie * kQueueDepth + (r.x & 1u)) * (uint64_t)c.qrec_dw,
+                               ABLATE(L, 16));
+        }
+        if (base + kQueueLanes >= cnt) break;
+      }
+      for (uint64_t st0 = tot + (uint64_t)jme * kQueueLanes; st0 < olen; st0 += (uint64_t)nj * kQueueLanes) {
+        const uint32_t m = (uint32_t)min((uint64_t)kQueueLanes, olen - st0);
+        made += m;
+        if ((uint32_t)lane < m) {
+          const uint2 r = ovf[st0 + lane];
           const uint64_t ie = r.x >> 1;
           gen_queue_entry<BIG>(c, S, ie, r.y, gplan, pdw, S.qbuf + (ie * kQueueDepth + (r.x & 1u)) * (uint64_t)c.qrec_dw,
                                ABLATE(L, 16));
@@ -3407,7 +3469,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   for (uint64_t blk = blockIdx.x; blk < nblk;) {
     STAMP(0);
     uint32_t got = 0xffffffffu;
-    if (tid == 0 && *qn + 2u * (uint32_t)L.envs <= cap) got = atomicAdd(&bctr[qsel & 3u], 1u);
+    if (tid == 0 && nblk > gridDim.x && *qn + 2u * (uint32_t)L.envs <= cap) got = atomicAdd(&bctr[qsel & 3u], 1u);
     // the per-lane values derive from an opaque copy of the lane id, block by block: hoisted out of
     // the loop, they and what the compiler derives from them would hold registers through every
     // block (the env waves spilled at 128 VGPRs)
@@ -3531,8 +3593,21 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       uint32_t base = 0;
       if (lane == 0) base = atomicAdd(qn, (uint32_t)__popcll(rb));
       base = __builtin_amdgcn_readfirstlane(base);
+      const uint32_t k = (uint32_t)__popcll(rb);
+      // one round: list positions >= kQueueLanes go to the overflow list
+      const uint32_t ovn = (one_round && base + k > (uint32_t)kQueueLanes) ? base + k - max(base, (uint32_t)kQueueLanes) : 0u;
+      uint32_t obase = 0;
+      if (ovn) {
+        if (lane == 0) obase = atomicAdd(&S.qctr[kQctrOvfLen + set_new * 8u + ox], ovn);
+        obase = __builtin_amdgcn_readfirstlane(obase);
+      }
       if (reset_now) {
-        req_new[base + __popcll(rb & ((1ull << lane) - 1ull))] = make_uint2((uint32_t)i << 1 | qh, k0 + 10u);
+        const uint32_t p = base + (uint32_t)__popcll(rb & ((1ull << lane) - 1ull));
+        const uint2 r = make_uint2((uint32_t)i << 1 | qh, k0 + 10u);
+        if (one_round && p >= (uint32_t)kQueueLanes)
+          S.qovf[((uint64_t)par * 8u + ox) * ocap + obase + (p - max(base, (uint32_t)kQueueLanes))] = r;
+        else
+          req_new[p] = r;
         S.qstate[i] = (uint8_t)(qh ^ 1u);  // (every env's byte instead: 403.3 vs 401.4 us)
       }
     }
@@ -3546,19 +3621,18 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       group_obs<BIG>(c, S, v, reset_now, st, oi, L, wave, lane, ctr, bar, np, rank, vw, false);
       if (reset_now) write_small_outputs(c, out, i, v, oi, false);
     }
+    if (tid == 0) *nxt = got;
     STAMP(30);
     sub_barrier(ctr, bar += (uint32_t)np);
     STAMP(31);
-    if (tid == 0) {
-      S.qctr[par * gridDim.x + blockIdx.x] = *qn;  // (every request of the block is in)
-      *nxt = got;
-    }
+    if (tid == 0)  // (every request of the block is in)
+      S.qctr[par * gridDim.x + blockIdx.x] = one_round ? min(*qn, (uint32_t)kQueueLanes) : *qn;
+    const uint32_t g = *nxt;  // (written before the last barrier, rewritten after the next block's first)
     if (out.obs && !ABLATE(L, 4))
       write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr, rank, nthr);
     if (tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
     if (blk == blockIdx.x) stagger_record(L, S, t_start);
     STAMP(6);
-    const uint32_t g = *nxt;  // (written before the last barrier; rewritten only after the next one)
     blk = g == 0xffffffffu ? nblk : (uint64_t)gridDim.x + g;
   }
 }
@@ -4254,6 +4328,10 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
   // map-queue entries in whole 128-byte lines, written whole: partly written lines cost the step
   // launch 37 us of its 425 (1 048 576 5x5 envs, 80-byte entries)
   c.qrec_dw = (c.plan_dq * 4 + 4 + 31) & ~31;
+#ifdef PGTG_TUNING
+  if (const char* e = getenv("PGTG_QPAD"))
+    if (!atoi(e)) c.qrec_dw = c.plan_dq * 4 + 4;
+#endif
   return 0;
 }
 
@@ -4546,7 +4624,8 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
   if (h->L.queue) {
     if ((rc = dalloc(h, &h->S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw)) || (rc = dalloc(h, &h->S.qstate, n)) ||
         (rc = dalloc(h, &h->S.qreq, 2 * h->q_grid * queue_req_cap((n + h->L.envs - 1) / h->L.envs, h->q_grid, h->L.envs))) ||
-        (rc = dalloc(h, &h->S.qctr, 2 * kMaxQueueGrid + 3))) {
+        (rc = dalloc(h, &h->S.qovf, 2 * 8 * ((h->q_grid + 7) / 8) * (uint64_t)h->L.envs)) ||
+        (rc = dalloc(h, &h->S.qctr, kQctrWords))) {
       g_create_err = h->err;
       pgtg_destroy(h);
       return rc;
@@ -4622,7 +4701,7 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
 // and the rings of the envs a reset gave new maps.
 static int queue_fill(pgtg_handle* h) {
   if (!h->L.queue || !h->S.qbuf) return PGTG_OK;
-  HIPCHK(h, hipMemsetAsync(h->S.qctr, 0, (2 * kMaxQueueGrid + 3) * sizeof(uint32_t), h->stream));
+  HIPCHK(h, hipMemsetAsync(h->S.qctr, 0, kQctrWords * sizeof(uint32_t), h->stream));
 #ifdef PGTG_TUNING
   if (const char* e = getenv("PGTG_QFILL"))
     if (!atoi(e)) return PGTG_OK;
@@ -5060,7 +5139,7 @@ int pgtg_load_state(pgtg_handle* h, const void* buf, uint64_t bytes) {
     off += s.bytes;
   }
   if (h->S.tr_count) HIPCHK(h, hipMemset(h->S.tr_count, 0, 2 * sizeof(uint32_t)));
-  if (h->S.qctr) HIPCHK(h, hipMemset(h->S.qctr, 0, (2 * kMaxQueueGrid + 3) * sizeof(uint32_t)));  // (dumped with full rings)
+  if (h->S.qctr) HIPCHK(h, hipMemset(h->S.qctr, 0, kQctrWords * sizeof(uint32_t)));  // (dumped with full rings)
   return PGTG_OK;
 }
 
