@@ -2729,6 +2729,7 @@ struct Lds {
   int lm_words;        // terminal-observation line mask words (0: test the selection bytes)
   int stagger;         // first-round start offsets (stagger_start) on
   int stagger_wgs;     // workgroups resident in the first round (blocks per CU x CUs)
+  int ramp_pct;        // the ramp, in percent of the last launch's first workgroup duration
   int img_in_traf;     // k_env with traffic: the whole workgroup's image in the (after the car pass dead)
                        // traffic region; the agent tile's counters and the reset hand-over words in hist
   int abl;             // diagnostic ablations (PGTG_TUNING builds only, PGTG_ABL; always 0 otherwise):
@@ -2790,10 +2791,12 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.queue = !c.need_car && c.n_rules == 0 && !c.fixed_map && !c.generic_channels && envs <= kBlock - 64 && l.sub_envs >= envs;
   l.stagger = 0;
   l.stagger_wgs = 0;
+  l.ramp_pct = 50;
   l.img_in_traf = 0;
   l.abl = 0;
 #ifdef PGTG_TUNING  // A/B and diagnostic builds only: the product library reads no environment
   if (const char* e = getenv("PGTG_ABL")) l.abl = atoi(e);
+  if (const char* e = getenv("PGTG_RAMP")) l.ramp_pct = atoi(e);
   if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);
   if (const char* e = getenv("PGTG_COMPACT")) l.compact = atoi(e);
   if (const char* e = getenv("PGTG_QUEUE")) l.queue = l.queue && atoi(e);
@@ -2888,7 +2891,7 @@ __device__ __forceinline__ uint64_t stagger_start(const Lds& L, const DevState& 
   if (!L.stagger) return 0;
   const uint64_t t0 = wall_clock64();
   if (blockIdx.x == 0 || blockIdx.x >= (unsigned)L.stagger_wgs) return t0;
-  const uint64_t span = min(S.wg_ticks[0] / 2ull, (unsigned long long)kStaggerMaxTicks);
+  const uint64_t span = min(S.wg_ticks[0] * (uint64_t)L.ramp_pct / 100ull, (unsigned long long)kStaggerMaxTicks);
   const uint64_t wait = span * blockIdx.x / (unsigned)L.stagger_wgs;
   while (wall_clock64() - t0 < wait) __builtin_amdgcn_s_sleep(16);
   return t0;
