@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PGTG_ABI_VERSION 6
+#define PGTG_ABI_VERSION 7
 
 /* status codes (Python facade maps them to the reference's exception types) */
 #define PGTG_OK 0
@@ -117,6 +117,8 @@ typedef struct {
   int32_t tune_car_slots;              /* car slots per env (>= 3 x capacity + 4; tests of the bound) */
   int32_t tune_kt_serial;              /* 1: initial traffic's per-car draws on one lane per env (the
                                           rejection fallback of the lane-parallel path; tests) */
+  int32_t tune_fault;                  /* tests of the error paths: bit 0 clears the path walk's north
+                                          mask (inconsistent masks -> PGTG_E_DEVICE, the launch finishes) */
 } PgtgConfig;
 
 /* Output buffers (device pointers, caller-owned, contiguous).  NULL = not produced. */
@@ -213,6 +215,20 @@ int pgtg_set_to_state(pgtg_handle* h, uint64_t env, int32_t x, int32_t y, int32_
 /* Replace the traffic rules of every env (add_traffic_rule / remove_traffic_rule,
  * environment.py:569-575); takes effect from the next step.  n_rules <= PGTG_MAX_RULES. */
 int pgtg_set_rules(pgtg_handle* h, const PgtgRule* rules, int32_t n_rules);
+/* FlattenObservation rows (pgtg/train.py:40; gymnasium's flatten of the Dict observation space of
+ * environment.py:415-441, keys in name order), written by k_flatten after every launch that writes the
+ * bound observation (step, reset, observe): per env, D = n_channels*win*win (+ 9) + 18 + 2 values
+ *   map channels in `order` (order[k] = channel of the k-th name-sorted key), win*win each, [x][y] |
+ *   next-subgoal one-hot at direction + 1 (9, only with use_next_subgoal_direction) |
+ *   position one-hot of x (9), of y (9) | velocity (2)
+ * as float32 (dtype 0) or int8 (dtype 1: exact, every value being 0/1 or a velocity) into flat_dev
+ * [N][D]; final_flat_dev [N][D] receives the terminal observations of the envs that finished in a step
+ * (their rows only; the other rows are left as they are).  Buffers 16-byte aligned; NULL, NULL = off.
+ * Needs the corresponding PgtgOutputs bound first; a sliding window of size >= 9 is refused
+ * (PGTG_E_UNSUPPORTED) as gymnasium's flatten raises for it.  No reference function: it replaces the
+ * FlattenObservation wrapper the reference's caller puts around each env. */
+int pgtg_set_flat_outputs(pgtg_handle* h, const int32_t* order, int32_t n_order, int32_t dtype, void* flat_dev,
+                          void* final_flat_dev);
 /* Re-emit the observation of every env into the bound outputs (after set_agent/add_car). */
 int pgtg_observe(pgtg_handle* h);
 /* Per-env uint64 digest of the car list into out_dev[N] (device; parity tests: the car term of
@@ -224,6 +240,10 @@ int pgtg_get_counters(pgtg_handle* h, uint64_t* env_steps, uint64_t* episodes);
  * waves; 0 for handles without the queue): a window's delta beside its episode delta shows that the
  * maps the episodes consumed were generated in the window.  Synchronises. */
 int pgtg_get_queue_maps(pgtg_handle* h, uint64_t* maps);
+/* Map-queue refill requests served from the overflow lists since create (step launches of one round
+ * of workgroups list at most 64 requests per workgroup; the rest go to lists shared by residue mod 8
+ * and are served by other workgroups' helper waves in the next launch).  Synchronises. */
+int pgtg_get_queue_overflow(pgtg_handle* h, uint64_t* served);
 /* Number of envs whose last step reported an error (PGTG_E_DONE / PGTG_E_MAP); synchronises. */
 int pgtg_error_count(pgtg_handle* h, uint64_t* n_errors, int32_t* first_code);
 /* Measured HBM denominator of the roofline: a 16-B/lane stream copy of `bytes` between two device

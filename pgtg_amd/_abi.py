@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 # PGTG_LIB selects another build of the same library (test variants, pgtg_amd/build.py VARIANTS)
 LIB_PATH = os.environ.get("PGTG_LIB") or os.path.join(PKG, "libpgtg_hip.so")
 
-PGTG_ABI_VERSION = 6
+PGTG_ABI_VERSION = 7
 MAX_TILES = 256
 MAX_CHANNELS = 128
 MAX_RULES = 8
@@ -32,7 +32,7 @@ EXPORTED = [
     "pgtg_get_map_plan", "pgtg_get_squares", "pgtg_set_rules", "pgtg_set_agent", "pgtg_add_car", "pgtg_observe", "pgtg_get_counters",
     "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_launch_info", "pgtg_occupancy", "pgtg_step_kernel", "pgtg_last_error", "pgtg_enable_timing",
     "pgtg_timing_read", "pgtg_measure_hbm", "pgtg_state_size", "pgtg_dump_state", "pgtg_load_state",
-    "pgtg_set_to_state", "pgtg_car_digest", "pgtg_get_queue_maps",
+    "pgtg_set_to_state", "pgtg_car_digest", "pgtg_get_queue_maps", "pgtg_get_queue_overflow", "pgtg_set_flat_outputs",
 ]
 
 
@@ -66,7 +66,7 @@ class PgtgConfig(C.Structure):
         ("autoreset", C.c_int32), ("max_episode_steps", C.c_int32), ("min_car_capacity", C.c_int32),
         ("tune_envs_per_block", C.c_int32), ("tune_obs_sub", C.c_int32), ("tune_kt_grid", C.c_int32),
         ("tune_kt_cap", C.c_int32), ("tune_kt_wpc", C.c_int32), ("tune_car_slots", C.c_int32),
-        ("tune_kt_serial", C.c_int32),
+        ("tune_kt_serial", C.c_int32), ("tune_fault", C.c_int32),
     ]
 
 
@@ -130,6 +130,8 @@ def lib():
         "pgtg_get_counters": ([vp, C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "pgtg_car_digest": ([vp, vp], C.c_int),
         "pgtg_get_queue_maps": ([vp, C.POINTER(u64)], C.c_int),
+        "pgtg_get_queue_overflow": ([vp, C.POINTER(u64)], C.c_int),
+        "pgtg_set_flat_outputs": ([vp, C.POINTER(C.c_int32), i32, i32, vp, vp], C.c_int),
         "pgtg_error_count": ([vp, C.POINTER(u64), C.POINTER(i32)], C.c_int),
         "pgtg_window": ([vp], C.c_int),
         "pgtg_num_envs": ([vp], u64),
@@ -140,7 +142,12 @@ def lib():
         "pgtg_timing_read": ([vp, C.POINTER(C.c_double), C.POINTER(u64), i32], C.c_int),
         "pgtg_enable_timing": ([vp, i32], C.c_int),
     }
+    # A/B runs against an older build of the library (tools/ab_multi.sh): PGTG_ABI_COMPAT names its ABI
+    # version; entry points it does not have are left unbound
+    compat = os.environ.get("PGTG_ABI_COMPAT")
     for name, (args, res) in sig.items():
+        if compat and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
@@ -162,13 +169,13 @@ def fill_rules(dst, rules) -> int:
     return len(rules)
 
 
-TUNE_KEYS = ("envs_per_block", "obs_sub", "kt_grid", "kt_cap", "kt_wpc", "car_slots", "kt_serial")
+TUNE_KEYS = ("envs_per_block", "obs_sub", "kt_grid", "kt_cap", "kt_wpc", "car_slots", "kt_serial", "fault")
 
 
 def config_struct(spec: "cfgmod.EnvSpec", autoreset: bool, max_episode_steps: int | None,
                   min_car_capacity: int = 0, tune: dict | None = None) -> PgtgConfig:
     c = PgtgConfig()
-    c.abi_version = PGTG_ABI_VERSION
+    c.abi_version = int(os.environ.get("PGTG_ABI_COMPAT") or PGTG_ABI_VERSION)
     c.width, c.height = spec.width, spec.height
     c.pct_connections = spec.pct_connections
     c.start_mode, c.goal_mode = spec.start_mode, spec.goal_mode

@@ -103,6 +103,7 @@ struct DevCfg {
   // per-tile arrays of maps up to 256 tiles, kept behind the fields every launch reads
   uint16_t fixed_plan[kMaxTiles];
   double ind_reward[kMaxTiles + 1];
+  int32_t tune_fault;  // PgtgConfig.tune_fault (tests of the kernels' error paths; 0 in every real config)
 };
 
 // Lane-indexed constant tables, copied once per workgroup into LDS (pgtg_env.hip): the head (sT:

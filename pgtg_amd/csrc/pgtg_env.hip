@@ -981,11 +981,16 @@ __device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, i
     front = nx;
   }
   STAMP(25);
+  if (c.tune_fault & 1) cN = mask_zero<M>();  // (test knob: masks that disagree with the layers)
+  // The walk is bounded: a shortest path moves at most nt - 1 times, and every tile it stands on must
+  // have a tile one layer closer.  Masks that disagree with the BFS layers (the round-4 1-wide edge
+  // directions did) end it with -1 (PGTG_E_DEVICE for the env) instead of a loop that never ends.
   int v = s, len = 1;
   if constexpr (sizeof(M) <= 8) {  // <= 64 tiles: the walk in registers, then the plan marks
     M pN = 0, pE = 0, pS = 0, pW = 0;
     while (v != g) {
       const M b = (M)1 << v;
+      if (len >= c.nt || !((cN | cE | cS | cW) & b)) return -1;
       if (cN & b) { pN |= b; v -= w; }
       else if (cE & b) { pE |= b; v += 1; }
       else if (cS & b) { pS |= b; v += w; }
@@ -1002,6 +1007,7 @@ __device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, i
     while (v != g) {
       uint32_t d;
       int nv;
+      if (len >= c.nt || !mask_get(cN | cE | cS | cW, v)) return -1;
       if (mask_get(cN, v)) { d = 1u; nv = v - w; }
       else if (mask_get(cE, v)) { d = 2u; nv = v + 1; }
       else if (mask_get(cS, v)) { d = 3u; nv = v + w; }
@@ -1567,14 +1573,14 @@ __device__ __forceinline__ int env_reset(const DevCfg& c, const DevState& S, uin
   v.sg = (uint32_t)st_t | (uint32_t)st_d << 8 | (uint32_t)gl_t << 16 | (uint32_t)gl_d << 24;
   STAMP(11);
   v.used = 0;
-  v.path_len = (uint32_t)len;
+  v.path_len = (uint32_t)max(len, 0);
   v.flags = 0;
   v.phase = 0;
   v.elapsed = 0;
   v.vx = v.vy = 0;
-  if (len == 0 || !((plan_exits(plan[st_t]) >> st_d) & 1u)) {
+  if (len <= 0 || !((plan_exits(plan[st_t]) >> st_d) & 1u)) {
     v.px = v.py = 0;
-    return PGTG_E_MAP;
+    return len < 0 ? PGTG_E_DEVICE : PGTG_E_MAP;  // (< 0: the path walk's masks were inconsistent)
   }
   // starters: the start tile's exit segment in the start direction, x-major (pgtg/map.py:31-34)
   int j = (int)pcg_int(map_rng, 3);
@@ -3231,10 +3237,11 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
   int st_t, st_d, gl_t, gl_d;
   uint64_t ix[4];
   generate_map<BIG>(c, BIG ? S.epk : sT.epk, map_rng, plan, st_t, st_d, gl_t, gl_d, ix);
-  const int len = compile_generated<BIG>(c, plan, st_t, gl_t, ix);
+  int len = compile_generated<BIG>(c, plan, st_t, gl_t, ix);
   int px = 0, py = 0, err = 0;
-  if (len == 0 || !((plan_exits(plan[st_t]) >> st_d) & 1u)) {
-    err = PGTG_E_MAP;
+  if (len <= 0 || !((plan_exits(plan[st_t]) >> st_d) & 1u)) {
+    err = len < 0 ? PGTG_E_DEVICE : PGTG_E_MAP;  // (< 0: the path walk's masks were inconsistent)
+    len = 0;
   } else {  // env_reset's starter square (pgtg/map.py:31-34)
     const int j = (int)pcg_int(map_rng, 3);
     const int tx = st_t % c.tw, ty = st_t / c.tw;
@@ -3415,7 +3422,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     STAMP(1);
     // the helper: the previous launch's requests, kQueueLanes at a time, until none is left
     uint16_t* gplan = reinterpret_cast<uint16_t*>(lds + L.gen_off + lane * pdw);
-    uint32_t made = 0;
+    uint32_t made = 0, ovs = 0;  // maps generated, of them overflow requests
     if (!ABLATE(L, 1)) {
       // one round: this helper's share of its residue's overflow list -- as many as its spare lanes,
       // after those of the workgroups before it (a prefix sum over their list lengths, no atomics:
@@ -3443,6 +3450,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
         const uint32_t oth = base == 0 ? on : 0u;
         if (own + oth == 0) break;
         made += own + oth;
+        ovs += oth;
         if ((uint32_t)lane < own + oth) {
           const uint2 r = (uint32_t)lane >= own ? ovf[ob + (lane - own)] : base == 0 ? r0 : req_old[base + lane];
           const uint64_t ie = r.x >> 1;
@@ -3454,6 +3462,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       for (uint64_t st0 = tot + (uint64_t)jme * kQueueLanes; st0 < olen; st0 += (uint64_t)nj * kQueueLanes) {
         const uint32_t m = (uint32_t)min((uint64_t)kQueueLanes, olen - st0);
         made += m;
+        ovs += m;
         if ((uint32_t)lane < m) {
           const uint2 r = ovf[st0 + lane];
           const uint64_t ie = r.x >> 1;
@@ -3463,6 +3472,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       }
     }
     if (lane == 0 && made) atomicAdd(&S.counters[2], (unsigned long long)made);  // maps generated
+    if (lane == 0 && ovs) atomicAdd(&S.counters[3], (unsigned long long)ovs);  // overflow requests served
     STAMP(7);
     return;
   }
@@ -3914,6 +3924,78 @@ __global__ void __launch_bounds__(256) k_car_digest(DevState S, uint64_t* __rest
   out[i] = d;
 }
 
+// FlattenObservation rows (pgtg/train.py:40 wraps the env in gymnasium's FlattenObservation, whose
+// flatten of the Dict space of environment.py:415-441 orders the keys by name): per env
+//   map channels in name order (win*win each, [x][y]) | next-subgoal one-hot at d + 1 (9, with
+//   use_next_subgoal_direction) | position one-hot of x (9) and of y (9) | velocity (2)
+// as float32 or int8 (every value is a 0/1 entry or a velocity), from the observation the step kernels
+// just wrote.  The N x D values are one flat array: a thread writes 16 consecutive bytes of it (4
+// float32 or 16 int8 values; rows need not be aligned), reading the obs bytes they come from.  `final`:
+// the terminal observations, written only on the rows of envs that finished this step.
+struct FlatArgs {
+  const uint8_t* obs;
+  const int32_t* pos;
+  const int32_t* vel;
+  const int32_t* nsd;
+  const uint8_t* term;
+  const uint8_t* trunc;
+  void* dst;
+  uint64_t n;
+  int32_t D, OB, w2, cw2, nsd_on, final;
+  uint8_t order[PGTG_MAX_CHANNELS];  // channel (in the observation) of the k-th name-sorted key
+};
+template <typename T>
+__device__ __forceinline__ T flat_value(const FlatArgs& a, uint64_t e, uint32_t j, uint32_t slot, uint32_t sq) {
+  if (j < (uint32_t)a.cw2) return (T)a.obs[e * (uint64_t)a.OB + (uint32_t)a.order[slot] * (uint32_t)a.w2 + sq];
+  int k = (int)(j - (uint32_t)a.cw2);
+  if (a.nsd_on) {
+    if (k < 9) return (T)(k == a.nsd[e] + 1 ? 1 : 0);
+    k -= 9;
+  }
+  if (k < 9) return (T)(k == a.pos[2 * e] ? 1 : 0);
+  if (k < 18) return (T)(k - 9 == a.pos[2 * e + 1] ? 1 : 0);
+  return (T)a.vel[2 * e + (k - 18)];
+}
+template <typename T>
+__global__ void __launch_bounds__(256) k_flatten(FlatArgs a) {
+  constexpr int G = 16 / sizeof(T);
+  const uint64_t total = a.n * (uint64_t)a.D;
+  const uint64_t g0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * G;
+  if (g0 >= total) return;
+  uint64_t e = g0 / (uint64_t)a.D;
+  uint32_t j = (uint32_t)(g0 - e * (uint64_t)a.D);
+  uint32_t slot = j < (uint32_t)a.cw2 ? j / (uint32_t)a.w2 : 0u, sq = j < (uint32_t)a.cw2 ? j - slot * (uint32_t)a.w2 : 0u;
+  bool keep0 = !a.final || (a.term[e] | a.trunc[e]);
+  T v[G];
+  bool keep[G];
+#pragma unroll
+  for (int u = 0; u < G; u++) {
+    keep[u] = g0 + u < total && keep0;
+    v[u] = keep[u] ? flat_value<T>(a, e, j, slot, sq) : (T)0;
+    // next element: the next square / channel / tail value, or the next env's row
+    if (++j == (uint32_t)a.D) {
+      j = slot = sq = 0u;
+      if (++e < a.n) keep0 = !a.final || (a.term[e] | a.trunc[e]);
+    } else if (++sq == (uint32_t)a.w2) {
+      sq = 0u;
+      slot++;
+    }
+  }
+  T* d = reinterpret_cast<T*>(a.dst) + g0;
+  bool all = true;
+#pragma unroll
+  for (int u = 0; u < G; u++) all = all && keep[u];
+  if (all) {
+    uint4 q;
+    __builtin_memcpy(&q, v, 16);
+    *reinterpret_cast<uint4*>(d) = q;
+  } else {
+#pragma unroll
+    for (int u = 0; u < G; u++)
+      if (keep[u]) d[u] = v[u];
+  }
+}
+
 __global__ void k_fill_seeds(uint64_t* seed, uint64_t n, uint64_t base, uint64_t offset) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) seed[i] = base + offset + i;
@@ -3957,6 +4039,11 @@ struct pgtg_handle {
   // k_envq: step launches so far (its request lists rotate per launch) and its persistent grid
   uint64_t q_launch = 0;
   uint64_t q_grid = 0;
+  // FlattenObservation rows after every launch (pgtg_set_flat_outputs): k_flatten's arguments
+  FlatArgs flat{};
+  void* flat_dst = nullptr;
+  void* final_flat_dst = nullptr;
+  int flat_dtype = 0;  // 0 float32, 1 int8
 };
 
 
@@ -4052,6 +4139,7 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
   c.W = tw * kTile;
   c.H = th * kTile;
   c.fixed_map = in.fixed_map;
+  c.tune_fault = in.tune_fault;
   if (in.fixed_map) {
     for (int t = 0; t < c.nt; t++) {
       uint32_t p = in.fm_exits[t] & 15u;
@@ -4513,7 +4601,8 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
   ALLOC(S.seed, n);
   ALLOC(S.plan, n * (uint64_t)c.plan_stride);
   ALLOC(S.err, n);
-  ALLOC(S.counters, 4);  // env steps, episodes, map-queue entries generated (state blob: the first two)
+  ALLOC(S.counters, 4);  // env steps, episodes, map-queue entries generated, overflow requests served
+                         // (state blob: the first two)
   ALLOC(S.wg_ticks, 1);
   DevStream* streams[4] = {&S.car, &S.ice, &S.broken, &S.sand};
   int needs[4] = {c.need_car, c.need_ice, c.need_broken, c.need_sand};
@@ -4660,6 +4749,26 @@ int pgtg_set_outputs(pgtg_handle* h, const PgtgOutputs* o) {
   return PGTG_OK;
 }
 
+// k_flatten over the bound observation (final: the terminal observations, finished envs' rows only)
+static int launch_flatten(pgtg_handle* h, bool final) {
+  FlatArgs a = h->flat;
+  const PgtgOutputs& o = h->out;
+  a.obs = final ? o.final_obs : o.obs;
+  a.pos = final ? o.final_position : o.position;
+  a.vel = final ? o.final_velocity : o.velocity;
+  a.nsd = final ? o.final_next_subgoal : o.next_subgoal;
+  a.term = o.terminated;
+  a.trunc = o.truncated;
+  a.dst = final ? h->final_flat_dst : h->flat_dst;
+  a.final = final ? 1 : 0;
+  const uint64_t chunks = (h->n * (uint64_t)a.D * (h->flat_dtype ? 1u : 4u) + 15) / 16;
+  const dim3 grid((unsigned)((chunks + 255) / 256));
+  if (h->flat_dtype) hipLaunchKernelGGL(k_flatten<int8_t>, grid, dim3(256), 0, h->stream, a);
+  else hipLaunchKernelGGL(k_flatten<float>, grid, dim3(256), 0, h->stream, a);
+  HIPCHK(h, hipGetLastError());
+  return PGTG_OK;
+}
+
 static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, int mode) {
   HIPCHK(h, hipSetDevice(h->device));
   uint64_t blocks = (h->n + h->L.envs - 1) / h->L.envs;
@@ -4693,6 +4802,12 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
                        h->S, h->out, h->tr_slot, h->kt_plan_dw, h->kt_rs_dw, h->kt_cap);
     HIPCHK(h, hipGetLastError());
     h->tr_slot ^= 1u;
+  }
+  if (h->flat_dst) {
+    if (int rc = launch_flatten(h, false)) return rc;
+  }
+  if (h->final_flat_dst && mode == MODE_STEP) {
+    if (int rc = launch_flatten(h, true)) return rc;
   }
   if (timed) {
     HIPCHK(h, hipEventRecord(h->evpool[h->ev_used + 1], h->stream));
@@ -5212,6 +5327,53 @@ int pgtg_get_queue_maps(pgtg_handle* h, uint64_t* maps) {
   unsigned long long c[3];
   HIPCHK(h, hipMemcpy(c, h->S.counters, sizeof c, hipMemcpyDeviceToHost));
   *maps = c[2];
+  return PGTG_OK;
+}
+
+int pgtg_set_flat_outputs(pgtg_handle* h, const int32_t* order, int32_t n_order, int32_t dtype, void* flat_dev,
+                          void* final_flat_dev) {
+  if (!h) return PGTG_E_INVALID;
+  h->flat_dst = h->final_flat_dst = nullptr;
+  if (!flat_dev && !final_flat_dev) return PGTG_OK;
+  const DevCfg& c = h->hcfg;
+  const PgtgOutputs& o = h->out;
+  if (dtype != 0 && dtype != 1) return fail(h, PGTG_E_INVALID, "flat dtype: 0 float32, 1 int8");
+  if (!order || n_order != c.n_channels) return fail(h, PGTG_E_INVALID, "flat order: one entry per channel");
+  uint64_t seen[2] = {0, 0};
+  for (int k = 0; k < n_order; k++) {
+    if (order[k] < 0 || order[k] >= n_order || ((seen[order[k] >> 6] >> (order[k] & 63)) & 1u))
+      return fail(h, PGTG_E_INVALID, "flat order: not a permutation of the channels");
+    seen[order[k] >> 6] |= 1ull << (order[k] & 63);
+  }
+  if (c.sliding && c.ss >= 9)  // gymnasium's flatten of MultiDiscrete([9, 9]) indexes past its 18 entries
+    return fail(h, PGTG_E_UNSUPPORTED, "position (s, s) of a sliding window of size >= 9 is outside MultiDiscrete([9, 9])");
+  if (flat_dev && (!o.obs || !o.position || !o.velocity || (c.next_subgoal && !o.next_subgoal)))
+    return fail(h, PGTG_E_INVALID, "flat rows need the obs, position, velocity (and next_subgoal) outputs");
+  if (final_flat_dev && (!o.final_obs || !o.final_position || !o.final_velocity || !o.terminated || !o.truncated ||
+                         (c.next_subgoal && !o.final_next_subgoal)))
+    return fail(h, PGTG_E_INVALID, "terminal flat rows need the final_* and terminated/truncated outputs");
+  if (((uintptr_t)flat_dev | (uintptr_t)final_flat_dev) & 15u) return fail(h, PGTG_E_INVALID, "flat rows: 16-byte aligned buffers");
+  FlatArgs& a = h->flat;
+  a.n = h->n;
+  a.w2 = c.win * c.win;
+  a.OB = c.obs_bytes;
+  a.cw2 = c.n_channels * a.w2;
+  a.nsd_on = c.next_subgoal ? 1 : 0;
+  a.D = a.cw2 + (a.nsd_on ? 9 : 0) + 20;
+  for (int k = 0; k < n_order; k++) a.order[k] = (uint8_t)order[k];
+  h->flat_dtype = dtype;
+  h->flat_dst = flat_dev;
+  h->final_flat_dst = final_flat_dev;
+  return PGTG_OK;
+}
+
+int pgtg_get_queue_overflow(pgtg_handle* h, uint64_t* served) {
+  if (!h || !served) return PGTG_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  unsigned long long c[4];
+  HIPCHK(h, hipMemcpy(c, h->S.counters, sizeof c, hipMemcpyDeviceToHost));
+  *served = c[3];
   return PGTG_OK;
 }
 

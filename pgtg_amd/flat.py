@@ -8,8 +8,10 @@ values.  For the PGTG space (environment.py:415-441) that is
     map/<features sorted by name> (w*w each) | next_subgoal_direction (9, one-hot of d+1) |
     position (9 + 9 one-hots) | velocity (2)
 
-`flatten_obs` builds that vector for every env of a batch directly from the device tensors of a
-`PGTGVecEnv` observation (no host round trip).
+`flatten_obs` builds that vector for every env of a batch from the device tensors of a `PGTGVecEnv`
+observation with torch ops (the reference formula the tests compare with); the product path writes
+the same rows with the HIP kernel `k_flatten` after every step (`PGTGVecEnv.set_flat_outputs`,
+include/pgtg.h `pgtg_set_flat_outputs`).
 """
 from __future__ import annotations
 
@@ -28,6 +30,20 @@ def flat_dim(spec) -> int:
     return sum(w for _, w in flat_layout(spec))
 
 
+def flat_order(spec) -> list[int]:
+    """order[k] = index in spec.channels (the observation's channel order) of the k-th key by name:
+    the channel permutation of the device flattener (include/pgtg.h pgtg_set_flat_outputs)."""
+    keys = [k for k, _ in spec.channels]
+    return sorted(range(len(keys)), key=lambda i: keys[i])
+
+
+def check_flattenable(spec) -> None:
+    """gymnasium's flatten raises for a sliding window of size >= 9 (see flatten_obs)."""
+    if spec.sliding and spec.sliding_size >= 9:
+        raise IndexError(f"position ({spec.sliding_size}, {spec.sliding_size}) is outside MultiDiscrete([9, 9]): "
+                         f"index {9 + spec.sliding_size} is out of bounds for its flattened size 18")
+
+
 def flatten_obs(spec, obs: dict, dtype=None):
     """obs: a PGTGVecEnv observation dict ({"map": {k: [N, w, w]}, "position": [N, 2], ...}) ->
     [N, flat_dim] tensor (float32 by default) on the same device."""
@@ -42,9 +58,7 @@ def flatten_obs(spec, obs: dict, dtype=None):
     # the agent's square in its tile (0..8) or, with a sliding window, (s, s) (environment.py:1453), so
     # a window of size s >= 9 puts 9 + s past the vector's end, where gymnasium's index assignment
     # raises -- as here, decided from the spec without reading the tensor.
-    if spec.sliding and spec.sliding_size >= 9:
-        raise IndexError(f"position ({spec.sliding_size}, {spec.sliding_size}) is outside MultiDiscrete([9, 9]): "
-                         f"index {9 + spec.sliding_size} is out of bounds for its flattened size 18")
+    check_flattenable(spec)
     oh = torch.zeros((n, 18), dtype=dtype, device=pos.device)
     oh.scatter_(1, torch.stack([pos[:, 0], 9 + pos[:, 1]], dim=1), 1)
     parts.append(oh)

@@ -7,16 +7,19 @@ pgtg/train.py:54-55).
 `infos[i]["TimeLimit.truncated"]` for finished envs (`infos` a lazy sequence, `VecInfos`: no per-env
 Python loop in the step).  Observations are the `FlattenObservation`
 vectors of pgtg/train.py:40 (pgtg_amd/flat.py), as float32 numpy arrays because SB3 policies take
-host arrays (views of two page-locked buffer sets used in turn: a step's arrays are valid until the
-step after next -- SB3's rollout buffer copies them at once); `max_episode_steps` is the `TimeLimit(100)` wrapper of pgtg/train.py:39, applied
-in-kernel (truncation and auto-reset in the same step).
+host arrays (views of page-locked buffers that are fresh for every step, so a caller may keep them like
+SubprocVecEnv's arrays; `zero_copy=True` reuses two buffer sets in turn, a step's arrays then being valid
+until the step after next); `max_episode_steps` is the `TimeLimit(100)` wrapper of pgtg/train.py:39,
+applied in-kernel (truncation and auto-reset in the same step).
 
 `device_obs=True` keeps everything on the env's GPU for device-side rollout buffers and policies:
 observations, rewards and dones come back as torch tensors (`obs_dtype`: float32 by default; int8 is
 exact as well, every flattened value being a 0/1 one-hot entry or a velocity in Box(-99, 99)),
 actions may be a device tensor, and the infos (`DeviceVecInfos`)
-carry the batch's terminal observations as one [N, D] tensor, converted to SB3's per-env dicts only
-if an entry is read.  Nothing crosses PCIe in the step.
+carry the batch's terminal observations as one [N, D] tensor (valid on the rows of finished envs),
+converted to SB3's per-env dicts only if an entry is read.  Nothing crosses PCIe in the step.  The
+flattened rows (float32 / int8) are written by the HIP kernel k_flatten inside the step (include/pgtg.h
+pgtg_set_flat_outputs) into tensors that are fresh for every step; other dtypes go through flatten_obs.
 """
 from __future__ import annotations
 
@@ -122,7 +125,7 @@ class DeviceVecInfos(Sequence):
 class PGTGSB3VecEnv:
     def __init__(self, num_envs: int, map_path: str | None = None, *, max_episode_steps: int | None = 100,
                  device: int | None = None, seed: int = 0, device_obs: bool = False, obs_dtype=None,
-                 **kwargs: Any):
+                 zero_copy: bool = False, **kwargs: Any):
         self.venv = PGTGVecEnv(num_envs, map_path, device=device, autoreset=True,
                                max_episode_steps=max_episode_steps, **kwargs)
         self.spec = self.venv.spec
@@ -131,6 +134,7 @@ class PGTGSB3VecEnv:
         self._seed = seed
         self._actions = None
         self.device_obs = bool(device_obs)
+        self.zero_copy = bool(zero_copy)
         self.obs_dtype = obs_dtype
         try:
             from gymnasium import spaces
@@ -145,9 +149,36 @@ class PGTGSB3VecEnv:
         self._seed = 0 if seed is None else int(seed)
         return [self._seed + i for i in range(self.num_envs)]
 
+    def _kernel_flat(self) -> bool:
+        """The rows come from the HIP flattener (the host path's float32, the device path's float32 /
+        int8); other device dtypes from flatten_obs."""
+        import torch
+        return not self.device_obs or self._dtype() in (torch.float32, torch.int8)
+
+    def _bind_flat(self, final: bool):
+        """Device rows for the next launch: fresh tensors on the device path (a step's tensors stay the
+        caller's), one persistent pair on the host path (copied to the host before step_wait returns)."""
+        import torch
+        if not self.device_obs:
+            if not hasattr(self, "_flat_d"):
+                shape = (self.num_envs, self.obs_dim)
+                self._flat_d = torch.empty(shape, dtype=torch.float32, device=self.venv.device)
+                self._final_d = torch.empty(shape, dtype=torch.float32, device=self.venv.device)
+                self.venv.set_flat_outputs(self._flat_d, self._final_d)
+            return self._flat_d, self._final_d
+        shape, dt = (self.num_envs, self.obs_dim), self._dtype()
+        flat = torch.empty(shape, dtype=dt, device=self.venv.device)
+        fin = torch.empty(shape, dtype=dt, device=self.venv.device) if final else None
+        self.venv.set_flat_outputs(flat, fin)
+        return flat, fin
+
     def reset(self):
-        obs, _ = self.venv.reset(seed=self._seed)
-        flat = flatten_obs(self.spec, obs, dtype=self._dtype())
+        if self._kernel_flat():
+            flat, _ = self._bind_flat(final=False)
+            self.venv.reset(seed=self._seed)
+        else:
+            obs, _ = self.venv.reset(seed=self._seed)
+            flat = flatten_obs(self.spec, obs, dtype=self._dtype())
         return flat if self.device_obs else flat.cpu().numpy()
 
     def _dtype(self):
@@ -162,7 +193,9 @@ class PGTGSB3VecEnv:
             # device actions: no host round trip and no range check (that would be a device sync per
             # step); an action outside Discrete(9) is recorded by the kernel per env (error_count())
             a = actions.reshape(self.num_envs)
-            self._actions = a if a.dtype == torch.uint8 else a.clamp(0, 255).to(torch.uint8)
+            if a.dtype != torch.uint8:  # every value outside Discrete(9) becomes the invalid code 255
+                a = torch.where((a < 0) | (a > 8), torch.full_like(a, 255), a).to(torch.uint8)
+            self._actions = a
             return
         a = np.asarray(actions.cpu() if isinstance(actions, torch.Tensor) else actions).reshape(self.num_envs)
         if a.size and (a.min() < 0 or a.max() > 8):  # an out-of-space action raises (environment.py:1118)
@@ -171,19 +204,28 @@ class PGTGSB3VecEnv:
 
     def step_wait(self):
         import torch
+        kflat = self._kernel_flat()
+        if kflat:
+            flat_d, final_d = self._bind_flat(final=True)
         obs, reward, term, trunc, infos = self.venv.step(self._actions)
         if self.device_obs:
-            dt = self._dtype()
-            dones = term.bool() | trunc.bool()
-            final = flatten_obs(self.spec, infos["final_observation"], dtype=dt)  # every row: no sync
+            dones = term | trunc
+            if kflat:  # written by k_flatten in the step: no torch work on the observations
+                flat, final = flat_d, final_d
+            else:
+                dt = self._dtype()
+                flat = flatten_obs(self.spec, obs, dtype=dt)
+                final = flatten_obs(self.spec, infos["final_observation"], dtype=dt)  # every row: no sync
             cost = infos.get("cost")
-            return (flatten_obs(self.spec, obs, dtype=dt), reward.to(torch.float32), dones,
-                    DeviceVecInfos(dones, trunc.bool() & ~term.bool(), final, cost))
-        # host arrays (SB3's VecEnv contract): one copy per step into page-locked buffers, two sets used
-        # in turn (the arrays a step returns stay valid through the next step), and the terminal
-        # observations of the finished envs only
+            if cost is not None:  # (the venv's output buffer, rewritten by the next step)
+                cost = cost.clone()
+            return (flat, reward.to(torch.float32), dones, DeviceVecInfos(dones, trunc & ~term, final, cost))
+        # host arrays (SB3's VecEnv contract): one copy per step into page-locked buffers, and the
+        # terminal observations of the finished envs only.  The buffers are fresh for every step (torch's
+        # caching host allocator: a block returns to the cache only when the arrays over it are dropped),
+        # so a caller may keep a step's arrays as long as it likes, as with SubprocVecEnv; zero_copy=True
+        # reuses two buffer sets in turn instead (a step's arrays are then valid until the step after next)
         h = self._host_buffers()
-        flat_d = flatten_obs(self.spec, obs)
         h["obs"].copy_(flat_d, non_blocking=True)
         h["rew"].copy_(reward.to(torch.float32), non_blocking=True)
         h["term"].copy_(term, non_blocking=True)
@@ -196,25 +238,30 @@ class PGTGSB3VecEnv:
         dones = term_h | trunc_h
         final, rows = None, None
         idx = np.nonzero(dones)[0]
-        if idx.size:
-            fin = flatten_obs(self.spec, infos["final_observation"])
-            final = fin.index_select(0, torch.as_tensor(idx, device=fin.device)).cpu().numpy()
+        if idx.size:  # (k_flatten wrote the finished envs' rows)
+            final = final_d.index_select(0, torch.as_tensor(idx, device=final_d.device)).cpu().numpy()
             rows = np.full(self.num_envs, -1, np.int64)
             rows[idx] = np.arange(idx.size)
         if "cost" in infos:
             cost = h["cost"].numpy().copy()
         return h["obs"].numpy(), h["rew"].numpy(), dones, VecInfos(dones, trunc_h & ~term_h, final, cost, rows)
 
-    def _host_buffers(self) -> dict:
+    def _new_host_buffers(self) -> dict:
         import torch
+
+        def pinned(shape, dtype):
+            return torch.empty(shape, dtype=dtype, pin_memory=True)
+        return {"obs": pinned((self.num_envs, self.obs_dim), torch.float32),
+                "rew": pinned((self.num_envs,), torch.float32),
+                "term": pinned((self.num_envs,), torch.uint8),
+                "trunc": pinned((self.num_envs,), torch.uint8),
+                "cost": pinned((self.num_envs,), torch.float64)}
+
+    def _host_buffers(self) -> dict:
+        if not self.zero_copy:
+            return self._new_host_buffers()
         if not hasattr(self, "_hbuf"):
-            def pinned(shape, dtype):
-                return torch.empty(shape, dtype=dtype, pin_memory=True)
-            self._hbuf = [{"obs": pinned((self.num_envs, self.obs_dim), torch.float32),
-                           "rew": pinned((self.num_envs,), torch.float32),
-                           "term": pinned((self.num_envs,), torch.uint8),
-                           "trunc": pinned((self.num_envs,), torch.uint8),
-                           "cost": pinned((self.num_envs,), torch.float64)} for _ in range(2)]
+            self._hbuf = [self._new_host_buffers() for _ in range(2)]
             self._flip = 0
         self._flip ^= 1
         return self._hbuf[self._flip]

@@ -222,6 +222,37 @@ class PGTGVecEnv:
         _check(self._lib.pgtg_step_many(self._h, C.c_void_p(actions.data_ptr()), actions.stride(0),
                                         actions.shape[0]), self._h)
 
+    def set_flat_outputs(self, flat=None, final_flat=None):
+        """Have every launch also write the FlattenObservation rows (pgtg/train.py:40) of the
+        observation into `flat` and, in steps, the finished envs' terminal rows into `final_flat`:
+        [N, flat_dim] float32 or int8 device tensors (include/pgtg.h pgtg_set_flat_outputs; the HIP
+        kernel k_flatten, no torch work).  Rebinding per step is cheap (the pointers are kept by the
+        handle); None, None turns it off."""
+        import torch
+
+        from .flat import check_flattenable, flat_dim, flat_order
+        bufs = [t for t in (flat, final_flat) if t is not None]
+        if not bufs:
+            _check(self._lib.pgtg_set_flat_outputs(self._h, None, 0, 0, None, None), self._h)
+            self._flat_refs = ()
+            return
+        check_flattenable(self.spec)
+        D = flat_dim(self.spec)
+        dt = bufs[0].dtype
+        for t in bufs:
+            if t.dtype not in (torch.float32, torch.int8) or t.dtype != dt:
+                raise ValueError("flat rows: float32 or int8 tensors, both of one dtype")
+            if tuple(t.shape) != (self.num_envs, D) or not t.is_contiguous() or t.device != self.device:
+                raise ValueError(f"flat rows: contiguous [{self.num_envs}, {D}] tensors on {self.device}")
+        if final_flat is not None and not self.autoreset:
+            raise ValueError("terminal flat rows need autoreset=True")
+        order = flat_order(self.spec)
+        arr = (C.c_int32 * len(order))(*order)
+        ptr = lambda x: None if x is None else C.c_void_p(x.data_ptr())  # noqa: E731
+        _check(self._lib.pgtg_set_flat_outputs(self._h, arr, len(order), 0 if dt == torch.float32 else 1,
+                                               ptr(flat), ptr(final_flat)), self._h)
+        self._flat_refs = (flat, final_flat)  # (the handle writes into them: keep them alive)
+
     def observe(self):
         """Re-emit every env's observation (after set_agent / add_car)."""
         self._bind_stream()
@@ -379,6 +410,14 @@ class PGTGVecEnv:
         """Map-queue ring entries generated since create (0 without the queue)."""
         m = C.c_uint64()
         _check(self._lib.pgtg_get_queue_maps(self._h, C.byref(m)), self._h)
+        return m.value
+
+    def queue_overflow(self) -> int:
+        """Map-queue refill requests served from the one-round overflow lists since create."""
+        m = C.c_uint64()
+        if not hasattr(self._lib, "pgtg_get_queue_overflow"):  # (an older build, tools/ab_multi.sh)
+            return -1
+        _check(self._lib.pgtg_get_queue_overflow(self._h, C.byref(m)), self._h)
         return m.value
 
     def enable_timing(self, every: int = 1):

@@ -9,6 +9,7 @@ formulas to each other), so whole batches are compared without copying them to t
   configs[4]  1 048 576 envs x 40 steps, 5x5 maps (the bench line; grid indexing past 2^20 envs; the
               map-queue rings through their refill steady state: a ring holds 3 episodes, a
               workgroup's helper wave refills <= 64 of them per launch)
+  configs[4]'s 8-GPU shard 131 072 envs x 40 steps (one round of workgroups: the overflow lists)
   configs[2]  65 536 envs x 200 steps, 5x5 maps, traffic 0.5, with every env's car list in the
               digest (id, square, route, profile, patience, delay of every car after every step: the
               persisted occupancy counters, packing ticks, patience past patience_level*10), plus
@@ -49,13 +50,13 @@ def _gpu_digests(spec, n, T, tune=None):
         for t in range(T):
             env.step_random(ACT_SEED, t)
             out[t] = dg.step_digest().cpu().numpy().view(np.uint64)
-        return out, env.step_kernel(), env.launch_info()
+        return out, env.step_kernel(), env.launch_info(), env.queue_overflow()
     finally:
         env.close()
 
 
 def _compare(spec, n, T, tune=None, tag="", min_distinct=1000):
-    got, kern, shape = _gpu_digests(spec, n, T, tune)
+    got, kern, shape, ovf = _gpu_digests(spec, n, T, tune)
     ref = oracle.rollout_digest(spec, n, T, ACT_SEED)
     # the comparison has teeth: the rollout visits many distinct outputs.  Observations are local
     # 9x9 windows, so envs on small maps share digests (3x3 maps: 4 096 envs x 100 steps give 7 326
@@ -63,6 +64,7 @@ def _compare(spec, n, T, tune=None, tag="", min_distinct=1000):
     assert len(np.unique(ref)) >= min(ref.size // 4, min_distinct), "degenerate digests"
     bad = np.argwhere(got != ref)
     assert bad.size == 0, (f"{tag} {kern} {shape}: {len(bad)} (step, env) digests differ, first {bad[:8].tolist()}")
+    return ovf
 
 
 # every feature name of the reference's vocabulary (pgtg/environment.py:1387-1445) plus names it does
@@ -124,6 +126,16 @@ CASES = {
 def test_every_env_every_step(name):
     n, T, kw, tune = CASES[name]
     _compare(_spec(kw), n, T, tune, name)
+
+
+@pytest.mark.timeout(600)
+def test_one_round_shard_overflow_path():
+    """configs[4]'s per-GPU shard at N = 8 (131 072 envs: one round of map-queue workgroups), every env
+    at every step.  In a one-round launch a workgroup lists at most 64 ring-refill requests; the rest go
+    to the overflow lists that other workgroups' helpers serve in the next launch (pgtg_env.hip k_envq).
+    The device counter of overflow requests served shows that this path ran in the compared rollout."""
+    ovf = _compare(_spec(dict(random_map_width=5, random_map_height=5)), 131072, 40, None, "cfg5_all_131072x40")
+    assert ovf > 0, "no overflow request was served: the one-round overflow path did not run"
 
 
 @pytest.mark.timeout(600)

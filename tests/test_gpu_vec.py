@@ -181,3 +181,69 @@ def test_step_kernel_occupancy(n, kw, want):
         assert vec.launch_info()[0] * vec.occupancy() >= want, (vec.launch_info(), vec.occupancy())
     finally:
         vec.close()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.int8])
+def test_flat_rows_kernel_equals_flatten_obs(dtype):
+    """k_flatten (include/pgtg.h pgtg_set_flat_outputs: the FlattenObservation rows written inside the
+    step) against flatten_obs, gymnasium's layout: every env's row of the observation after reset and
+    each of 30 steps, and the terminal rows of the finished envs (the others untouched), on the
+    caller's settings (pgtg/train.py:21-40) with the default feature list, whose name order differs
+    from the observation's channel order, over a multi-workgroup batch."""
+    from pgtg_amd.flat import flat_dim
+    from pgtg_amd.vector import PGTGVecEnv
+    spec = _spec(random_map_width=4, random_map_height=4, random_map_obstacle_probability=0.2,
+                 random_map_percentage_of_connections=0.8, traffic_density=0.2, use_sliding_observation_window=True,
+                 sliding_observation_window_size=5, use_next_subgoal_direction=True)
+    assert [k for k, _ in spec.channels] != sorted(k for k, _ in spec.channels)
+    N, T = 3000, 30
+    env = PGTGVecEnv(N, spec=spec, device=0, autoreset=True, max_episode_steps=7)
+    D = flat_dim(spec)
+    flat = torch.empty((N, D), dtype=dtype, device="cuda")
+    fin = torch.full((N, D), 77, dtype=dtype, device="cuda")
+    env.set_flat_outputs(flat, fin)
+    env.reset(seed=11)
+    assert torch.equal(flat, flatten_obs(spec, env.observation(), dtype=dtype))
+    g = torch.Generator(device="cuda").manual_seed(4)
+    finished = 0
+    for t in range(T):
+        fin.fill_(77)
+        env.step(torch.randint(0, 9, (N,), device="cuda", dtype=torch.uint8, generator=g))
+        assert torch.equal(flat, flatten_obs(spec, env.observation(), dtype=dtype)), t
+        done = env.terminated | env.truncated
+        want = flatten_obs(spec, env.final_observation(), dtype=dtype)
+        assert torch.equal(fin[done], want[done]), t
+        assert bool((fin[~done] == 77).all()), t
+        finished += int(done.sum())
+    assert finished > N
+    env.close()
+
+
+def test_flat_rows_refused_where_gymnasium_raises():
+    from pgtg_amd.flat import flat_dim
+    from pgtg_amd.vector import PGTGVecEnv
+    spec = _spec(random_map_width=3, random_map_height=3, use_sliding_observation_window=True,
+                 sliding_observation_window_size=9)
+    env = PGTGVecEnv(4, spec=spec, device=0)
+    with pytest.raises(IndexError):
+        env.set_flat_outputs(torch.empty((4, flat_dim(spec)), device="cuda"))
+    env.close()
+
+
+def test_sb3_device_actions_out_of_range_are_recorded():
+    """A device action outside Discrete(9) (e.g. -1 from an int64 policy output) is never mapped onto a
+    valid action: the kernel records PGTG_E_INVALID for that env (error_count())."""
+    from pgtg_amd import _abi
+    from pgtg_amd.sb3 import PGTGSB3VecEnv
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        env = PGTGSB3VecEnv(8, max_episode_steps=5, seed=1, device_obs=True, random_map_width=3, random_map_height=3)
+    env.reset()
+    a = torch.zeros(8, dtype=torch.int64, device="cuda")
+    a[3], a[5] = -1, 9
+    env.step(a)
+    n, code = env.venv.error_count()
+    assert n == 2 and code == _abi.PGTG_E_INVALID
+    env.step(torch.full((8,), 4, dtype=torch.int64, device="cuda"))
+    assert env.venv.error_count()[0] == 0
+    env.close()
