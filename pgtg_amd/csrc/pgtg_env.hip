@@ -981,7 +981,7 @@ __device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, i
     front = nx;
   }
   STAMP(25);
-  if (c.tune_fault & 1) cN = mask_zero<M>();  // (test knob: masks that disagree with the layers)
+  if ((c.tune_fault & 1) && (s & 1)) cN = mask_zero<M>();  // (test knob: masks that disagree with the layers)
   // The walk is bounded: a shortest path moves at most nt - 1 times, and every tile it stands on must
   // have a tile one layer closer.  Masks that disagree with the BFS layers (the round-4 1-wide edge
   // directions did) end it with -1 (PGTG_E_DEVICE for the env) instead of a loop that never ends.

@@ -1,8 +1,9 @@
 """Error paths of the kernels: a data-dependent loop whose exit depends on the consistency of the
 map masks must end the launch with an error for the env, never spin (the round-4
 library's path walk hung on inconsistent 1-wide edge directions).  The test knob tune_fault bit 0
-(include/pgtg.h) clears the path walk's north mask, so every path that needs a north move finds no
-direction: those envs report PGTG_E_DEVICE, the others run normally, and every launch finishes."""
+(include/pgtg.h) clears the path walk's north mask on maps with an odd start tile index, so those
+paths that need a north move find no direction: those envs report PGTG_E_DEVICE, the others run
+normally, and every launch finishes."""
 import warnings
 
 import pytest

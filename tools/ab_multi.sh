@@ -7,6 +7,7 @@
 #                                                   writes, 4 no observation writes; timing only)
 #   new:--kt-wpc=2                                 k_traffic workgroups per CU
 #   new:--envs-per-block=64:--envs=131072          launch shape at a shard size
+#   ab/old.so:PGTG_ABI_COMPAT=6:--envs=131072       a build of an older ABI version (pgtg_amd/_abi.py)
 # Modes (environment): AB_STEPS / AB_WARMUP the bench window (100 / 20); AB_KTRACE=1 per-kernel
 # rocprofv3 averages (k_env, k_traffic separately) instead of the bench line; AB_RAMP=1 the
 # per-launch kernel time of the first 80 launches after a reset (tools/ramp.py) instead.

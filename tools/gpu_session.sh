@@ -11,10 +11,12 @@
 #   benchlong:<wl>   bench.py --workload <wl> with the default 1000-step window
 #   rccl             bench.py under torch.distributed.run, one rank, nccl backend, --dist (RCCL init +
 #                    the device counter all-reduce), 131 072 envs
-#   ranks            2 and 4 ranks on one GPU (gloo) at the full configs[4] batch, per-env digests vs one process
+#   ranks            2, 4 and 8 ranks on one GPU (gloo) at the full configs[4] batch (8 ranks: the 131 072-env
+#                    one-round shard of an 8-GPU run), per-env digests vs one process
 #   shards           single-process lines at the per-rank shards of N = 2, 4, 8 (524 288 / 262 144 /
 #                    131 072 envs) beside the 1 048 576-env line
 #   adapter          bench.py --adapter device / host / host-monitor (the SB3 VecEnv adapter, caller workload)
+#   hwid3            wave-to-SIMD placement of four resident 256-thread workgroups per CU (tools/micro/hwid3)
 #   profile:<wl,..>  tools/gpu_profile.sh (rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes)
 #   genbench         map-generation latency per map (tools/genbench.py, stamps build)
 #   stamps:<wl,..>   per-phase cycle stamps (PGTG_STAMPS build, tools/stamps.py)
@@ -68,7 +70,7 @@ for S in "$@"; do
       # the sharded path rehearsed on one GPU: 2 and 4 ranks (gloo counters, every rank on GPU 0) at the full
       # configs[4] batch; every rank's per-env output digests against the single-process run's
       timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 --no-cpu-baseline --digest $O/dg1 > $O/ranks_1.json 2> $O/ranks_1.err || { tail -20 $O/ranks_1.err; exit 1; }
-      for N in 2 4; do
+      for N in 2 4 8; do
         PGTG_BENCH_SAME_GPU=1 PGTG_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node $N --master-addr 127.0.0.1 --master-port $((29600 + N)) bench.py --gpus $N --steps 30 \
           --warmup 10 --no-cpu-baseline --digest $O/dg$N > $O/ranks_$N.json 2> $O/ranks_$N.err || { tail -30 $O/ranks_$N.err; exit 1; }
@@ -85,6 +87,9 @@ for S in "$@"; do
         timeout -k 10 300 python -u bench.py --adapter $M --steps 200 --warmup 20 > $O/adapter_$M.json 2> $O/adapter_$M.err || { tail -20 $O/adapter_$M.err; exit 1; }
         python -c "import json; d=json.load(open('$O/adapter_$M.json')); print('$M', round(d['value'] / 1e6, 2), 'M env-steps/s', round(d['ms_per_step'], 2), 'ms/step')"
       done ;;
+    hwid3)
+      timeout -k 10 60 ./tools/micro/hwid3 > $O/hwid3.log 2>&1 || { tail -20 $O/hwid3.log; exit 1; }
+      grep -v amdgpu.ids $O/hwid3.log ;;
     profile:*)
       R=${S#profile:}; timeout -k 10 1500 bash tools/gpu_profile.sh $TAG ${R//,/ } > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
       tail -5 $O/profile.log ;;
