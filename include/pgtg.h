@@ -118,7 +118,7 @@ typedef struct {
   int32_t tune_kt_serial;              /* 1: initial traffic's per-car draws on one lane per env (the
                                           rejection fallback of the lane-parallel path; tests) */
   int32_t tune_fault;                  /* tests of the error paths: bit 0 clears the path walk's north
-                                          mask on maps whose start tile index is odd (inconsistent masks ->
+                                          mask on maps whose tile 0 keeps its east exit (inconsistent masks ->
                                           PGTG_E_DEVICE for those envs, the launch finishes) */
 } PgtgConfig;
 

@@ -56,8 +56,15 @@ def build(force: bool = False, verbose: bool = False, variant: str | None = None
     return out
 
 
+def build_all(force: bool = False, verbose: bool = False, variants=tuple(VARIANTS)) -> list[str]:
+    """The product library and the given variants, compiled concurrently (one hipcc each)."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=1 + len(variants)) as ex:
+        futs = [ex.submit(build, force, verbose, v) for v in (None, *variants)]
+        return [f.result() for f in futs]
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
-    for v in VARIANTS:
-        build(force="--force" in sys.argv, verbose=True, variant=v)
-    print(OUT)
+    tools = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--tools=")]
+    print("\n".join(build_all(force="--force" in sys.argv, verbose=True,
+                               variants=tuple(VARIANTS) + tuple(tools[0] if tools else ()))))

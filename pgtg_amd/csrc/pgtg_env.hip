@@ -981,7 +981,8 @@ __device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, i
     front = nx;
   }
   STAMP(25);
-  if ((c.tune_fault & 1) && (s & 1)) cN = mask_zero<M>();  // (test knob: masks that disagree with the layers)
+  // (test knob: masks that disagree with the layers, on the maps whose tile 0 keeps its east exit)
+  if ((c.tune_fault & 1) && mask_get(hE, 0)) cN = mask_zero<M>();
   // The walk is bounded: a shortest path moves at most nt - 1 times, and every tile it stands on must
   // have a tile one layer closer.  Masks that disagree with the BFS layers (the round-4 1-wide edge
   // directions did) end it with -1 (PGTG_E_DEVICE for the env) instead of a loop that never ends.
@@ -2741,7 +2742,8 @@ struct Lds {
   int abl;             // diagnostic ablations (PGTG_TUNING builds only, PGTG_ABL; always 0 otherwise):
                        // k_envq bit 0 no ring refills (the stale entries taken as they are), bit 1 no
                        // terminal-observation writes, bit 2 no observation writes, bit 4 refills without
-                       // the ring-entry stores, bit 5 no plan-row stores at resets (timing experiments:
+                       // the ring-entry stores, bit 5 no plan-row stores at resets, bit 6 the env waves
+                       // take their own ring heads (the round-5 layout; a valid A/B) (timing experiments:
                        // the results are wrong)
 };
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
@@ -3367,6 +3369,48 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
   }
 }
 
+// A reset's ring take: the head entry of env i's ring (slot qh, made for spawn counter k0) becomes its
+// episode -- the tile plan into its HBM row and its LDS row, the obstacle streams of the episode, and
+// {px | py << 16, start/goal word, path length | error << 16} returned (env_reset without the generation).
+template <bool BIG>
+__device__ __forceinline__ uint3 ring_take(const DevCfg& c, const DevState& S, const Lds& L, uint64_t i, uint32_t qh,
+                                           uint32_t k0, uint32_t* plan_w, int pdw) {
+  const uint4* q4 = reinterpret_cast<const uint4*>(S.qbuf + (i * kQueueDepth + qh) * (uint64_t)c.qrec_dw);
+  uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
+  // all loads of the entry first: a load after a store to S.plan (which the compiler cannot
+  // tell apart from the queue) would wait for the one before it, one HBM latency per 16 bytes
+  const int nq = c.plan_dq;  // 16-byte words of the tile plan (<= 8 unless BIG)
+  const uint4 meta = q4[nq];
+  for (int k0q = 0; k0q < (BIG ? nq : 1); k0q += 8) {
+    uint4 qw[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) qw[k] = q4[k0q + k < nq ? k0q + k : k0q];  // unconditional: registers, not scratch
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (k0q + k < nq) {
+        if (!ABLATE(L, 32)) dstp[k0q + k] = qw[k];
+        const uint32_t wv[4] = {qw[k].x, qw[k].y, qw[k].z, qw[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if ((k0q + k) * 4 + j < pdw) plan_w[(k0q + k) * 4 + j] = wv[j];
+      }
+    }
+  }
+  if (!ABLATE(L, 32))
+    for (int k = nq; k < c.plan_stride / 8; k++) dstp[k] = make_uint4(0u, 0u, 0u, 0u);  // the row's whole lines
+  if (c.need_ice || c.need_broken || c.need_sand) {
+    SeedPool sp = ss_pool(S.seed[i]);
+    if (c.need_ice) stream_store_all(S.ice, i, ss_child(sp, k0 + 2u));
+    if (c.need_broken) stream_store_all(S.broken, i, ss_child(sp, k0 + 3u));
+    if (c.need_sand) stream_store_all(S.sand, i, ss_child(sp, k0 + 4u));
+  }
+  // the entry was generated for this episode (spawn counter k0): every launch serves all of the
+  // previous launch's requests and the ring holds two entries, so it always is -- a mismatch is
+  // reported as a device error, never used
+  const int e2 = (meta.w != queue_tag(k0) && !ABLATE(L, 1 | 16)) ? PGTG_E_DEVICE : -(int)(meta.z >> 16);
+  return make_uint3(meta.x, meta.y, (meta.z & 0xffffu) | (uint32_t)(-e2) << 16);
+}
+
 template <bool BIG>
 __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
                                                     DevState S, const uint8_t* __restrict__ actions, PgtgOutputs out,
@@ -3376,6 +3420,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint64_t t_start = stagger_start(L, S);
   STAMP(0);  // (the env waves' is each block's start)
+  STAMPR(2);  // (wall clock: every wave's start and end, slots 2 and 3 -- the launch's ramp and tail)
   const int env_waves = (L.envs + 63) / 64, gen_wave = env_waves;
   const bool env_wave = wave < env_waves;
   // refill requests: this launch's into list qsel & 3 (buffer qsel >> 2), the previous launch's from
@@ -3474,12 +3519,15 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     if (lane == 0 && made) atomicAdd(&S.counters[2], (unsigned long long)made);  // maps generated
     if (lane == 0 && ovs) atomicAdd(&S.counters[3], (unsigned long long)ovs);  // overflow requests served
     STAMP(7);
+    STAMPR(3);
     return;
   }
 
   // ---- env and writer waves (all but the helper), block after block ----
   const int np = kBlock / 64 - 1;  // participating waves
   const int nthr = np * 64;
+  // the last wave (neither env nor helper when a block has <= 128 envs) takes the ring heads
+  const bool taker_on = env_waves <= 2 && !ABLATE(L, 64);
   uint32_t bar = 0;  // running sub_barrier target
   for (uint64_t blk = blockIdx.x; blk < nblk;) {
     STAMP(0);
@@ -3537,62 +3585,55 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       if (live) write_small_outputs(c, out, i, v, oi, my_sel == 1);
     }
     if (env_wave) sel[slot] = my_sel;
+    // the take's hand-over words of a finished env: its spawn counter and ring head in, the entry out
+    uint32_t* xs = lds + L.envs * pdw + (env_wave ? slot : 0) * L.scratch_dw;
+    if (taker_on && my_sel == 1) {
+      xs[0] = v.spawn;
+      xs[1] = qh;
+    }
     const uint64_t rm = __ballot(my_sel == 1);
     if (env_wave && lane == 0 && rm) atomicAdd(&S.counters[1], (unsigned long long)__popcll(rm));
     STAMP(2);
     STAMP(28);
     sub_barrier(ctr, bar += (uint32_t)np);
     STAMP(29);
-    if (out.final_obs && !ABLATE(L, 2))
-      write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, rank, nthr, lm);
+    if (taker_on && wave == kBlock / 64 - 1) {
+      // The taker wave loads the finished envs' ring heads while the others write the terminal lines:
+      // the env waves then read their new episodes from LDS.  (A wave's loads are waited for together
+      // with every store it issued before them -- gfx9's vmcnt counts both in order -- so the env waves'
+      // own takes after their terminal stores waited for those stores to drain.)
+      const uint64_t m0 = __ballot(lane < nb && sel[lane] == 1);
+      const uint64_t m1 = __ballot(64 + lane < nb && sel[min(64 + lane, kBlock - 1)] == 1);
+      const int n0 = __popcll(m0), nf = n0 + __popcll(m1);
+      for (int j = lane; j < nf; j += 64) {
+        const int e = j < n0 ? select64(m0, j) : 64 + select64(m1, j - n0);
+        uint32_t* xe = lds + L.envs * pdw + e * L.scratch_dw;
+        const uint3 tk = ring_take<BIG>(c, S, L, env0 + e, xe[1], xe[0], lds + e * pdw, pdw);
+        xe[0] = tk.x;
+        xe[1] = tk.y;
+        xe[2] = tk.z;
+      }
+    } else if (out.final_obs && !ABLATE(L, 2)) {
+      write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, rank,
+                taker_on ? nthr - 64 : nthr, lm);
+    }
     STAMP(3);
-    sub_barrier(ctr, bar += (uint32_t)np);  // terminal images written before they are rebuilt
+    sub_barrier(ctr, bar += (uint32_t)np);  // terminal images written before they are rebuilt (and the takes in)
     const bool reset_now = my_sel != 0;
     const uint32_t k0 = v.spawn;
     if (reset_now) {  // the ring's head becomes the episode (env_reset without the generation)
-      const uint4* q4 = reinterpret_cast<const uint4*>(S.qbuf + (i * kQueueDepth + qh) * (uint64_t)c.qrec_dw);
-      uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
-      // all loads of the entry first: a load after a store to S.plan (which the compiler cannot
-      // tell apart from the queue) would wait for the one before it, one HBM latency per 16 bytes
-      const int nq = c.plan_dq;  // 16-byte words of the tile plan (<= 8 unless BIG)
-      const uint4 meta = q4[nq];
-      for (int k0q = 0; k0q < (BIG ? nq : 1); k0q += 8) {
-        uint4 qw[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) qw[k] = q4[k0q + k < nq ? k0q + k : k0q];  // unconditional: registers, not scratch
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          if (k0q + k < nq) {
-            if (!ABLATE(L, 32)) dstp[k0q + k] = qw[k];
-            const uint32_t wv[4] = {qw[k].x, qw[k].y, qw[k].z, qw[k].w};
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-              if ((k0q + k) * 4 + j < pdw) plan_w[(k0q + k) * 4 + j] = wv[j];
-          }
-        }
-      }
-      if (!ABLATE(L, 32))
-        for (int k = nq; k < c.plan_stride / 8; k++) dstp[k] = make_uint4(0u, 0u, 0u, 0u);  // the row's whole lines
-      if (c.need_ice || c.need_broken || c.need_sand) {
-        SeedPool sp = ss_pool(S.seed[i]);
-        if (c.need_ice) stream_store_all(S.ice, i, ss_child(sp, k0 + 2u));
-        if (c.need_broken) stream_store_all(S.broken, i, ss_child(sp, k0 + 3u));
-        if (c.need_sand) stream_store_all(S.sand, i, ss_child(sp, k0 + 4u));
-      }
+      const uint3 tk = taker_on ? make_uint3(xs[0], xs[1], xs[2]) : ring_take<BIG>(c, S, L, i, qh, k0, plan_w, pdw);
       v.spawn = k0 + 5u;
-      v.sg = meta.y;
+      v.sg = tk.y;
       v.used = 0;
-      v.path_len = meta.z & 0xffffu;
+      v.path_len = tk.z & 0xffffu;
       v.flags = 0;
       v.phase = 0;
       v.elapsed = 0;
       v.vx = v.vy = 0;
-      v.px = (int)(int16_t)(meta.x & 0xffffu);
-      v.py = (int)(int16_t)(meta.x >> 16);
-      // the entry was generated for this episode (spawn counter k0): every launch serves all of the
-      // previous launch's requests and the ring holds two entries, so it always is -- a mismatch is
-      // reported as a device error, never used
-      const int e2 = (meta.w != queue_tag(k0) && !ABLATE(L, 1 | 16)) ? PGTG_E_DEVICE : -(int)(meta.z >> 16);
+      v.px = (int)(int16_t)(tk.x & 0xffffu);
+      v.py = (int)(int16_t)(tk.x >> 16);
+      const int e2 = -(int)(tk.z >> 16);
       if (e2) err = e2;
       if (S.visited && e2 == 0) {
         uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
@@ -3650,6 +3691,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     STAMP(6);
     blk = g == 0xffffffffu ? nblk : (uint64_t)gridDim.x + g;
   }
+  STAMPR(3);
 }
 
 // Fill every env's map ring: after a reset launch (whose k_env generated the current episodes' maps
@@ -4424,6 +4466,8 @@ static int derive_cfg(pgtg_handle* h, const PgtgConfig& in, DevCfg& c) {
 #ifdef PGTG_TUNING
   if (const char* e = getenv("PGTG_QPAD"))
     if (!atoi(e)) c.qrec_dw = c.plan_dq * 4 + 4;
+  if (const char* e = getenv("PGTG_PPAD"))
+    if (!atoi(e)) c.plan_stride = c.plan_dq * 8;
 #endif
   return 0;
 }

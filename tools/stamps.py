@@ -117,6 +117,18 @@ for name in (sys.argv[1:] or ["cfg2", "cfg5"]):
                   "(the traffic_reset stamps are the last round's)", flush=True)
             print("  k_traffic waves (mean, p90, max): total", q(tot), "before the last round", q(pro),
                   "last round's traffic_reset", q(body), "epilogue", q(epi), flush=True)
+    rt = buf[1 << 20:(1 << 20) + 8 * nw].reshape(nw, 8).astype(np.int64)
+    okw = (rt[:, 2] > 0) & (rt[:, 3] > rt[:, 2])
+    if not spread and okw.any():  # k_envq: wall-clock start and end of every wave (10 ns ticks, one clock)
+        wid = np.arange(nw)[okw]
+        t0 = rt[okw, 2].min()
+        beg, end = rt[okw, 2] - t0, rt[okw, 3] - t0
+        hw = (wid % 4) * 64 == ((E + 63) // 64) * 64
+        ew = (wid % 4) * 64 < E
+        q = lambda a: (int(a.mean()), int(np.percentile(a, 50)), int(np.percentile(a, 90)), int(a.max()))  # noqa: E731
+        print("  wall clock (10 ns ticks from the first wave's start; mean, p50, p90, max): wave starts", q(beg),
+              "env-wave ends", q(end[ew]) if ew.any() else None, "helper ends", q(end[hw]) if hw.any() else None,
+              "writer-wave ends", q(end[~ew & ~hw]) if (~ew & ~hw).any() else None, flush=True)
     if not spread:  # k_envq env waves: the observation channel loop's split (slots 24, 25)
         okc = (st[:, 24] > 0) & (st[:, 24] < 1e7) & (st[:, 25] < 1e7)
         if okc.any():
