@@ -256,6 +256,8 @@ def main():
     ap.add_argument("--envs-per-block", type=int, default=0, help="A/B: force the step kernel's envs per workgroup")
     ap.add_argument("--kt-wpc", type=int, default=0, help="A/B: k_traffic workgroups per CU")
     ap.add_argument("--kt-cap", type=int, default=0, help="A/B: k_traffic envs per wave held in LDS")
+    ap.add_argument("--queue-mode", type=int, default=0,
+                    help="A/B: map-queue step kernel (0 automatic, 1 k_envq persistent, 2 k_envb per block)")
     ap.add_argument("--adapter", choices=["host", "host-monitor", "device"], default="",
                     help="time the SB3 VecEnv adapter (pgtg_amd/sb3.py) instead: PGTGSB3VecEnv.step over "
                          "the caller workload (pgtg/train.py's settings), host numpy or device-tensor path; "
@@ -299,7 +301,7 @@ def main():
     shard = Shard(rank, world, n_local)
     peak_copy = measure_hbm(local) if rank == 0 else 0.0
     tune = {k: v for k, v in (("envs_per_block", args.envs_per_block), ("kt_wpc", args.kt_wpc),
-                              ("kt_cap", args.kt_cap)) if v} or None
+                              ("kt_cap", args.kt_cap), ("queue_mode", args.queue_mode)) if v} or None
     env = PGTGVecEnv(n_local, spec=spec, device=local, autoreset=True, max_episode_steps=max_steps, tune=tune)
     env.reset(seed=shard.offset)  # global env g = rank*n_local + i gets seed g
     act_seed = 0x5EED

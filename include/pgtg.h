@@ -117,6 +117,8 @@ typedef struct {
   int32_t tune_car_slots;              /* car slots per env (>= 3 x capacity + 4; tests of the bound) */
   int32_t tune_kt_serial;              /* 1: initial traffic's per-car draws on one lane per env (the
                                           rejection fallback of the lane-parallel path; tests) */
+  int32_t tune_queue_mode;             /* map-queue step kernel: 0 automatic (k_envb for grids of <= 2 rounds
+                                          of workgroups, else k_envq), 1 k_envq, 2 k_envb */
   int32_t tune_fault;                  /* tests of the error paths: bit 0 clears the path walk's north
                                           mask on maps whose tile 0 keeps its east exit (inconsistent masks ->
                                           PGTG_E_DEVICE for those envs, the launch finishes) */

@@ -66,7 +66,7 @@ class PgtgConfig(C.Structure):
         ("autoreset", C.c_int32), ("max_episode_steps", C.c_int32), ("min_car_capacity", C.c_int32),
         ("tune_envs_per_block", C.c_int32), ("tune_obs_sub", C.c_int32), ("tune_kt_grid", C.c_int32),
         ("tune_kt_cap", C.c_int32), ("tune_kt_wpc", C.c_int32), ("tune_car_slots", C.c_int32),
-        ("tune_kt_serial", C.c_int32), ("tune_fault", C.c_int32),
+        ("tune_kt_serial", C.c_int32), ("tune_queue_mode", C.c_int32), ("tune_fault", C.c_int32),
     ]
 
 
@@ -169,7 +169,7 @@ def fill_rules(dst, rules) -> int:
     return len(rules)
 
 
-TUNE_KEYS = ("envs_per_block", "obs_sub", "kt_grid", "kt_cap", "kt_wpc", "car_slots", "kt_serial", "fault")
+TUNE_KEYS = ("envs_per_block", "obs_sub", "kt_grid", "kt_cap", "kt_wpc", "car_slots", "kt_serial", "queue_mode", "fault")
 
 
 def config_struct(spec: "cfgmod.EnvSpec", autoreset: bool, max_episode_steps: int | None,

@@ -2766,7 +2766,8 @@ __host__ __device__ inline uint64_t queue_req_cap(uint64_t nblk, uint64_t grid, 
   return c < (uint64_t)kQueueLanes ? (uint64_t)kQueueLanes : c;  // (the helper reads its first kQueueLanes ahead)
 }
 constexpr uint64_t kStaggerMaxTicks = 20000;  // 200 us of 100 MHz wall clock: a bound, never reached
-constexpr int kQueueDepth = 2;   // queued maps per env (a ring: the next two episodes')
+constexpr int kQueueDepth = 2;   // queued maps per env (a ring: the next two episodes') of k_envq
+constexpr int kBlockDepth = 3;   // of k_envb (the rings refilled per block)
 constexpr uint32_t kQueueStale = 0x80u;  // qstate flag: the ring's entries are not this env's (k_qfill)
 constexpr int kViewDw = 8;       // k_envq with <= 32 envs: an env's view words for the image builders
 
@@ -3374,8 +3375,8 @@ __device__ __forceinline__ void group_obs(const DevCfg& c, const DevState& S, co
 // {px | py << 16, start/goal word, path length | error << 16} returned (env_reset without the generation).
 template <bool BIG>
 __device__ __forceinline__ uint3 ring_take(const DevCfg& c, const DevState& S, const Lds& L, uint64_t i, uint32_t qh,
-                                           uint32_t k0, uint32_t* plan_w, int pdw) {
-  const uint4* q4 = reinterpret_cast<const uint4*>(S.qbuf + (i * kQueueDepth + qh) * (uint64_t)c.qrec_dw);
+                                           uint32_t k0, uint32_t* plan_w, int pdw, int depth = kQueueDepth) {
+  const uint4* q4 = reinterpret_cast<const uint4*>(S.qbuf + (i * (uint64_t)depth + qh) * (uint64_t)c.qrec_dw);
   uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
   // all loads of the entry first: a load after a store to S.plan (which the compiler cannot
   // tell apart from the queue) would wait for the one before it, one HBM latency per 16 bytes
@@ -3404,9 +3405,9 @@ __device__ __forceinline__ uint3 ring_take(const DevCfg& c, const DevState& S, c
     if (c.need_broken) stream_store_all(S.broken, i, ss_child(sp, k0 + 3u));
     if (c.need_sand) stream_store_all(S.sand, i, ss_child(sp, k0 + 4u));
   }
-  // the entry was generated for this episode (spawn counter k0): every launch serves all of the
-  // previous launch's requests and the ring holds two entries, so it always is -- a mismatch is
-  // reported as a device error, never used
+  // the entry was generated for this episode (spawn counter k0): k_envq serves every request of a
+  // launch in the next one and its ring holds two entries, k_envb refills every empty head before the
+  // take, so it always is -- a mismatch is reported as a device error, never used
   const int e2 = (meta.w != queue_tag(k0) && !ABLATE(L, 1 | 16)) ? PGTG_E_DEVICE : -(int)(meta.z >> 16);
   return make_uint3(meta.x, meta.y, (meta.z & 0xffffu) | (uint32_t)(-e2) << 16);
 }
@@ -3694,6 +3695,227 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   STAMPR(3);
 }
 
+// Step launch with the map queue for grids of at most two rounds of workgroups (k_envb: the map
+// queue per block).  Each workgroup steps its own block once; its helper wave refills the block's
+// rings from the ring states the env waves staged in LDS -- the heads of empty rings first (the env
+// waves wait for those at one barrier), then the second and third entries of the rings that need
+// them, at most kQueueLanes per launch (the rest wait for a later launch: a ring of three entries
+// has the slack).  No request lists, no block counter, no overflow lists: at one or two rounds each
+// helper's fill is on the launch's path, and these measured faster than k_envq's there (131 072 5x5
+// envs: 71.7-73.4 against 78.6-80.8 us per launch, 262 144: 131.5-132.1 against 142.2-143.2 us,
+// configs[1]'s 4 096 3x3 envs: 20.1 against 22.2 us; profiles/r06/s2/), while k_envq's persistent grid
+// wins from four rounds on.  qstate = entries held | head slot << 2.
+template <bool BIG>
+__global__ void __launch_bounds__(kBlock, 4) k_envb(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
+                                                    DevState S, const uint8_t* __restrict__ actions, PgtgOutputs out,
+                                                    Lds L) {
+  extern __shared__ uint32_t lds[];
+  const DevCfg& c = *cfg;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint64_t t_start = stagger_start(L, S);
+  STAMP(0);
+  STAMPR(2);  // (wall clock: every wave's start and end, slots 2 and 3)
+  stage_tables(gtab, false);  // (the map queue runs without lane channels: no sTX reference here)
+  const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
+  const int nb = (int)min((uint64_t)L.envs, S.n - env0);
+  const int env_waves = (L.envs + 63) / 64, gen_wave = env_waves;
+  // ring entries of levels 1.. regenerated per launch: one per helper lane, two with three env waves
+  // (192 envs reset ~80 times per launch at configs[4]'s rate)
+  const int qcap = env_waves > 2 ? 2 * kQueueLanes : kQueueLanes;
+  const bool env_wave = wave < env_waves;
+  const int slot = tid;
+  const uint64_t i = env0 + slot;
+  const bool live = env_wave && slot < nb;
+  const int pdw = L.plan_stride_dw;
+  uint32_t* plan_w = lds + (env_wave ? slot : 0) * pdw;
+  uint32_t* xf = lds + L.envs * pdw;  // per env slot: spawn counter, ring state at launch start
+  uint32_t* st = lds + L.envs * (pdw + L.scratch_dw + L.traf_dw + L.hist_dw);
+  uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
+  uint64_t* fm = reinterpret_cast<uint64_t*>(sel + kBlock);  // [level][env wave]: envs refilled at ring level
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(fm + 3 * kBlockDepth);  // sub_barrier counter
+  uint32_t* lm = L.lm_words ? reinterpret_cast<uint32_t*>(sel + kBlock + 128) : nullptr;  // terminal lines
+  uint32_t* vw = reinterpret_cast<uint32_t*>(sel + kBlock + 128) + L.lm_words;  // env views (<= 32 envs)
+  Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
+
+  EnvView v{};
+  uint32_t qs = 0;
+  int act = 0;
+  if (live) {
+    v = rec_load(S.rec, i);
+    qs = S.qstate[i];
+    act = actions[i];  // issued with the staging loads, not on the step's chain
+    stage_plan<BIG>(S.plan + i * (uint64_t)c.plan_stride, c.plan_dq, plan_w, pdw);
+    xf[slot * L.scratch_dw] = v.spawn;
+    xf[slot * L.scratch_dw + 1] = qs;
+  }
+  const uint32_t qn = qs & 3u, qh = (qs >> 2) & 3u;
+  if (env_wave) {  // refills: ring level l (0 = head) for the envs holding <= l maps
+#pragma unroll
+    for (int l = 0; l < kBlockDepth; l++) {
+      const uint64_t m = __ballot(live && qn <= (uint32_t)l);
+      if (lane == 0) fm[l * 3 + wave] = m;
+    }
+  }
+  if (tid == 0) *ctr = 0u;
+  for (int k = tid; k < L.lm_words; k += kBlock) lm[k] = 0u;
+  lds_barrier();  // tables, plans, refill masks, counter, line mask
+  STAMP(1);
+  // refills: the heads of empty rings (level 0, all of them), then levels 1.. in order (the first
+  // kQueueLanes this launch; the rest wait for a later launch)
+  int F[kBlockDepth];
+#pragma unroll
+  for (int l = 0; l < kBlockDepth; l++) {
+    F[l] = 0;
+    for (int w = 0; w < env_waves; w++) F[l] += __popcll(fm[l * 3 + w]);
+  }
+  const bool any_empty = F[0] != 0;
+#ifdef PGTG_STAMPS
+  if ((threadIdx.x & 63) == 0)  // diagnostic: empty rings and level-1/2 refills wanted in this workgroup
+    g_stamps[((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 32 + 12) & ((1 << 21) - 1)] =
+        (unsigned long long)F[0] | (unsigned long long)F[1] << 16 | (unsigned long long)F[2] << 32;
+#endif
+
+  if (wave == gen_wave) {
+    uint16_t* gplan = reinterpret_cast<uint16_t*>(lds + L.gen_off + lane * pdw);
+    auto refill = [&](int k, int l) {
+      int e = 0, pre = 0;
+      for (int w = 0; w < env_waves; w++) {
+        const uint64_t m = fm[l * 3 + w];
+        const int cw = __popcll(m);
+        if (k >= pre && k < pre + cw) e = w * 64 + select64(m, k - pre);
+        pre += cw;
+      }
+      const uint64_t ie = env0 + e;
+      const uint32_t qe = xf[e * L.scratch_dw + 1];
+      const uint32_t rslot = (((qe >> 2) & 3u) + (uint32_t)l) % (uint32_t)kBlockDepth;
+      gen_queue_entry<BIG>(c, S, ie, xf[e * L.scratch_dw] + 5u * (uint32_t)l, gplan, pdw,
+                      S.qbuf + (ie * kBlockDepth + rslot) * (uint64_t)c.qrec_dw, ABLATE(L, 16));
+    };
+    if (ABLATE(L, 1)) {
+      if (any_empty) __syncthreads();
+      return;
+    }
+    for (int k = lane; k < F[0]; k += kQueueLanes) refill(k, 0);  // every empty ring's head
+    if (any_empty) __syncthreads();  // head refills visible to the other waves
+    for (int k0 = lane; k0 < qcap; k0 += kQueueLanes) {  // levels 1.. in list order, up to qcap entries
+      int k = k0, l = 1;
+      while (l < kBlockDepth && k >= F[l]) {
+        k -= F[l];
+        l++;
+      }
+      if (l < kBlockDepth) refill(k, l);
+    }
+    if (lane == 0) {  // maps generated (S.counters[2]): the heads, then up to qcap for levels 1..
+      int rest = 0;
+      for (int l = 1; l < kBlockDepth; l++) rest += F[l];
+      atomicAdd(&S.counters[2], (unsigned long long)(F[0] + min(rest, qcap)));
+    }
+    STAMP(7);
+    STAMPR(3);
+    return;
+  }
+
+  // ---- env and writer waves (all but the refill wave) ----
+  const int np = kBlock / 64 - 1;                            // participating waves
+  const int rank = (wave < gen_wave ? wave : wave - 1) * 64 + lane, nthr = np * 64;
+  uint32_t bar = 0;  // running sub_barrier target
+  uint8_t my_sel = 0;
+  int err = 0;
+  if (live) {
+    StepResult res{0.0, 0.0, 0u};
+    bool occ_sat = false;
+    TrafState ts{0, 0, 0, 0};
+    err = env_step<false, BIG>(c, S, i, v, pl, act, res, nullptr, occ_sat, nullptr, ts, nullptr);
+    STAMP(22);
+    const bool done = (v.flags & (kFlagTerminated | kFlagTruncated)) != 0;
+    if (out.reward) out.reward[i] = res.reward;
+    if (out.cost) out.cost[i] = res.cost;
+    if (out.terminated) out.terminated[i] = (v.flags & kFlagTerminated) ? 1 : 0;
+    if (out.truncated) out.truncated[i] = (v.flags & kFlagTruncated) ? 1 : 0;
+    if (out.braking) out.braking[i] = 0;
+    my_sel = (done && c.autoreset && err == 0) ? 1 : 0;
+    if (BIG && res.plan_dirty && !my_sel) store_plan_row(c, S, i, plan_w, pdw);  // used subgoals (kPlanUsed)
+    if (lm && my_sel && out.final_obs) mark_lines(lm, out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)slot, (uint32_t)c.obs_bytes);
+    STAMP(23);
+  }
+  // the post-step image of every env (terminal for the finished ones)
+  {
+    ObsInfo oi;
+    group_obs<BIG>(c, S, v, live, st, oi, L, wave, lane, ctr, bar, np, rank, vw);
+    if (live) write_small_outputs(c, out, i, v, oi, my_sel == 1);
+  }
+  if (env_wave) sel[slot] = my_sel;
+  const uint64_t rm = __ballot(my_sel == 1);
+  if (env_wave && lane == 0 && rm) atomicAdd(&S.counters[1], (unsigned long long)__popcll(rm));
+  STAMP(2);
+  STAMP(28);
+  sub_barrier(ctr, bar += (uint32_t)np);
+  STAMP(29);
+  if (out.final_obs && !ABLATE(L, 2))
+    write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, rank, nthr, lm);
+  STAMP(3);
+  sub_barrier(ctr, bar += (uint32_t)np);  // terminal images written before they are rebuilt
+  if (any_empty) __syncthreads();  // the head refills
+  const bool reset_now = my_sel != 0;
+  if (reset_now) {  // the ring's head becomes the episode (env_reset without the generation)
+    const uint32_t k0 = v.spawn;
+    const uint3 tk = ring_take<BIG>(c, S, L, i, qh, k0, plan_w, pdw, kBlockDepth);
+    v.spawn = k0 + 5u;
+    v.sg = tk.y;
+    v.used = 0;
+    v.path_len = tk.z & 0xffffu;
+    v.flags = 0;
+    v.phase = 0;
+    v.elapsed = 0;
+    v.vx = v.vy = 0;
+    v.px = (int)(int16_t)(tk.x & 0xffffu);
+    v.py = (int)(int16_t)(tk.x >> 16);
+    const int e2 = -(int)(tk.z >> 16);
+    if (e2) err = e2;
+    if (S.visited && e2 == 0) {
+      uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
+      for (int q2 = 0; q2 < c.vis_words; q2++) vis[q2] = 0;
+      int b = (v.px + 2) * c.vis_pitch + (v.py + 2);
+      vis[b >> 5] |= 1u << (b & 31);
+    }
+  }
+  STAMP(4);
+  if (live) {
+    rec_store(S.rec, i, v);
+    S.err[i] = (uint8_t)(-err);
+    // ring entries after this launch: the refills served (same list order as the refill wave)
+    // minus the head a reset took
+    uint32_t have = qn == 0u ? 1u : qn;
+    int base = 0;  // list index of the first item of the level
+#pragma unroll
+    for (int l = 1; l < kBlockDepth; l++) {
+      int pre = 0;
+      for (int w = 0; w < wave; w++) pre += __popcll(fm[l * 3 + w]);
+      if (qn <= (uint32_t)l && base + pre + __popcll(fm[l * 3 + wave] & ((1ull << lane) - 1ull)) < qcap) have++;
+      base += F[l];
+    }
+    const uint32_t nq = reset_now ? have - 1u : have;  // have >= 1: every head is refilled
+    const uint32_t nh = reset_now ? (qh + 1u) % (uint32_t)kBlockDepth : qh;
+    S.qstate[i] = (uint8_t)(nq | nh << 2);
+  }
+  STAMP(5);
+  {
+    ObsInfo oi;
+    group_obs<BIG>(c, S, v, reset_now, st, oi, L, wave, lane, ctr, bar, np, rank, vw, false);
+    if (reset_now) write_small_outputs(c, out, i, v, oi, false);
+  }
+  STAMP(30);
+  sub_barrier(ctr, bar += (uint32_t)np);
+  STAMP(31);
+  if (out.obs && !ABLATE(L, 4))
+    write_obs(out.obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, nullptr, rank, nthr);
+  if (tid == 0) atomicAdd(&S.counters[0], (unsigned long long)nb);
+  stagger_record(L, S, t_start);
+  STAMP(6);
+  STAMPR(3);
+}
+
+
 // Fill every env's map ring: after a reset launch (whose k_env generated the current episodes' maps
 // and marked the reset envs' rings stale), a state dump (the requests still pending) or a change of
 // step kernel.  One lane per env checks both entries' spawn tags against the env's next two episodes
@@ -3724,6 +3946,35 @@ __global__ void __launch_bounds__(kBlock) k_qfill(const DevCfg* __restrict__ cfg
       }
     }
     if (stale) S.qstate[i] = 0;
+  }
+  // maps generated (S.counters[2]): one atomic per wave
+  const uint32_t wsum = (uint32_t)__popcll(__ballot(made & 1u)) + 2u * (uint32_t)__popcll(__ballot(made & 2u));
+  if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(&S.counters[2], (unsigned long long)wsum);
+}
+
+// k_qfill for k_envb's rings (three entries; qstate = held | head << 2, kQueueStale: none held): the
+// missing entries of every ring, levels held .. 2, the maps k_envb's helpers would generate.
+template <bool BIG>
+__global__ void __launch_bounds__(kBlock) k_qfill_b(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
+                                                    DevState S, int pdw) {
+  extern __shared__ uint32_t lds[];
+  const DevCfg& c = *cfg;
+  stage_tables(gtab, false);
+  lds_barrier();
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  uint32_t made = 0;
+  if (i < S.n) {
+    const uint32_t qs = S.qstate[i];
+    const uint32_t qn = (qs & kQueueStale) ? 0u : (qs & 3u), qh = (qs & kQueueStale) ? 0u : ((qs >> 2) & 3u);
+    if (qn < (uint32_t)kBlockDepth) {
+      const uint32_t spawn = S.rec[i].b.y;  // EnvRec w5
+      uint16_t* plan = reinterpret_cast<uint16_t*>(lds + threadIdx.x * pdw);
+      for (uint32_t l = qn; l < (uint32_t)kBlockDepth; l++)
+        gen_queue_entry<BIG>(c, S, i, spawn + 5u * l, plan, pdw,
+                             S.qbuf + (i * kBlockDepth + (qh + l) % (uint32_t)kBlockDepth) * (uint64_t)c.qrec_dw);
+      S.qstate[i] = (uint8_t)((uint32_t)kBlockDepth | qh << 2);
+      made = (uint32_t)kBlockDepth - qn;
+    }
   }
   // maps generated (S.counters[2]): one atomic per wave
   const uint32_t wsum = (uint32_t)__popcll(__ballot(made & 1u)) + 2u * (uint32_t)__popcll(__ballot(made & 2u));
@@ -4081,6 +4332,9 @@ struct pgtg_handle {
   // k_envq: step launches so far (its request lists rotate per launch) and its persistent grid
   uint64_t q_launch = 0;
   uint64_t q_grid = 0;
+  // map-queue step kernel, fixed at create: 1 k_envb (<= 2 rounds of workgroups), 0 k_envq, -1 not yet
+  int q_block = -1;
+  int tune_queue_mode = 0;  // PgtgConfig.tune_queue_mode
   // FlattenObservation rows after every launch (pgtg_set_flat_outputs): k_flatten's arguments
   FlatArgs flat{};
   void* flat_dst = nullptr;
@@ -4094,9 +4348,15 @@ struct pgtg_handle {
 static const void* step_fn(const pgtg_handle* h, int mode) {
   const bool big = h->hcfg.nt > kSmallTiles;
   if (h->hcfg.need_car || h->hcfg.n_rules > 0) return big ? (const void*)k_env<true, true> : (const void*)k_env<true, false>;
-  if (mode == MODE_STEP && h->L.queue) return big ? (const void*)k_envq<true> : (const void*)k_envq<false>;
+  if (mode == MODE_STEP && h->L.queue) {
+    if (h->q_block == 1) return big ? (const void*)k_envb<true> : (const void*)k_envb<false>;
+    return big ? (const void*)k_envq<true> : (const void*)k_envq<false>;
+  }
   return big ? (const void*)k_env<false, true> : (const void*)k_env<false, false>;
 }
+
+// entries per env ring of this handle's map queue (k_envb 3, k_envq 2)
+static int queue_depth(const pgtg_handle* h) { return h->q_block == 1 ? kBlockDepth : kQueueDepth; }
 
 static thread_local std::string g_create_err;
 
@@ -4580,7 +4840,8 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
   if (h->lds + sizeof(Tables) > 160 * 1024) return fail(h, PGTG_E_UNSUPPORTED, "LDS budget exceeded");
   if (h->lds > 64 * 1024) {
     const void* fns[] = {(const void*)k_env<true, false>, (const void*)k_env<false, false>, (const void*)k_envq<false>,
-                         (const void*)k_env<true, true>, (const void*)k_env<false, true>, (const void*)k_envq<true>};
+                         (const void*)k_env<true, true>, (const void*)k_env<false, true>, (const void*)k_envq<true>,
+                         (const void*)k_envb<false>, (const void*)k_envb<true>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
   }
   // first-round start offsets (stagger_start) for the launches without traffic
@@ -4599,6 +4860,11 @@ static int choose_launch(pgtg_handle* h, bool allow_queue) {
     // (more, with the later ones waiting for a slot: 125 % of them 429 vs 424 us per 1 048 576-env
     // launch, 150 % 450 us)
     h->q_grid = std::max<uint64_t>(1, std::min(std::min(blocks, (uint64_t)h->L.stagger_wgs), (uint64_t)kMaxQueueGrid));
+    // the map queue's step kernel, once per handle (its ring layout follows): k_envb for grids of at
+    // most two rounds of workgroups, k_envq's persistent grid beyond
+    if (h->q_block < 0 && h->L.queue)
+      h->q_block = h->tune_queue_mode ? (h->tune_queue_mode == 2 ? 1 : 0)
+                                      : (blocks <= (uint64_t)2 * h->L.stagger_wgs ? 1 : 0);
 #ifdef PGTG_TUNING
     if (const char* e = getenv("PGTG_STAGGER")) h->L.stagger = atoi(e);
 #endif
@@ -4617,6 +4883,7 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
   h->tune_kt_grid = cfg->tune_kt_grid;
   h->tune_kt_cap = cfg->tune_kt_cap;
   h->tune_kt_wpc = cfg->tune_kt_wpc;
+  h->tune_queue_mode = cfg->tune_queue_mode;
   int rc = 0;
   if (n_envs == 0) rc = fail(h, PGTG_E_INVALID, "n_envs must be > 0");
   if (!rc) rc = derive_cfg(h, *cfg, h->hcfg);
@@ -4760,10 +5027,11 @@ int pgtg_create(const PgtgConfig* cfg, uint64_t n_envs, int32_t device, pgtg_han
     return rc;
   }
   if (h->L.queue) {
-    if ((rc = dalloc(h, &h->S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw)) || (rc = dalloc(h, &h->S.qstate, n)) ||
-        (rc = dalloc(h, &h->S.qreq, 2 * h->q_grid * queue_req_cap((n + h->L.envs - 1) / h->L.envs, h->q_grid, h->L.envs))) ||
-        (rc = dalloc(h, &h->S.qovf, 2 * 8 * ((h->q_grid + 7) / 8) * (uint64_t)h->L.envs)) ||
-        (rc = dalloc(h, &h->S.qctr, kQctrWords))) {
+    if ((rc = dalloc(h, &h->S.qbuf, n * (uint64_t)queue_depth(h) * (uint64_t)c.qrec_dw)) || (rc = dalloc(h, &h->S.qstate, n)) ||
+        (!h->q_block &&
+         ((rc = dalloc(h, &h->S.qreq, 2 * h->q_grid * queue_req_cap((n + h->L.envs - 1) / h->L.envs, h->q_grid, h->L.envs))) ||
+          (rc = dalloc(h, &h->S.qovf, 2 * 8 * ((h->q_grid + 7) / 8) * (uint64_t)h->L.envs)) ||
+          (rc = dalloc(h, &h->S.qctr, kQctrWords))))) {
       g_create_err = h->err;
       pgtg_destroy(h);
       return rc;
@@ -4830,7 +5098,10 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
   }
   const void* fn = step_fn(h, mode);
   void* args[] = {&h->dcfg, &h->dtab, &h->S, &actions, &mask, &h->out, &mode, &h->L, &h->tr_slot};
-  if (fn == (const void*)k_envq<false> || fn == (const void*)k_envq<true>) {
+  if (fn == (const void*)k_envb<false> || fn == (const void*)k_envb<true>) {
+    void* bargs[] = {&h->dcfg, &h->dtab, &h->S, &actions, &h->out, &h->L};
+    HIPCHK(h, hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(kBlock), bargs, h->lds, h->stream));
+  } else if (fn == (const void*)k_envq<false> || fn == (const void*)k_envq<true>) {
     uint32_t qsel = (uint32_t)(h->q_launch % 3) | (uint32_t)(h->q_launch & 1) << 2;
     h->q_launch++;
     void* qargs[] = {&h->dcfg, &h->dtab, &h->S, &actions, &h->out, &h->L, &qsel};
@@ -4865,14 +5136,16 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
 // and the rings of the envs a reset gave new maps.
 static int queue_fill(pgtg_handle* h) {
   if (!h->L.queue || !h->S.qbuf) return PGTG_OK;
-  HIPCHK(h, hipMemsetAsync(h->S.qctr, 0, kQctrWords * sizeof(uint32_t), h->stream));
+  if (h->S.qctr) HIPCHK(h, hipMemsetAsync(h->S.qctr, 0, kQctrWords * sizeof(uint32_t), h->stream));
 #ifdef PGTG_TUNING
   if (const char* e = getenv("PGTG_QFILL"))
     if (!atoi(e)) return PGTG_OK;
 #endif
   const int pdw = h->L.plan_stride_dw;
   const size_t lds = (size_t)4 * kBlock * pdw;
-  const void* fn = h->hcfg.nt > kSmallTiles ? (const void*)k_qfill<true> : (const void*)k_qfill<false>;
+  const bool big = h->hcfg.nt > kSmallTiles;
+  const void* fn = h->q_block == 1 ? (big ? (const void*)k_qfill_b<true> : (const void*)k_qfill_b<false>)
+                                   : (big ? (const void*)k_qfill<true> : (const void*)k_qfill<false>);
   if (lds > 64 * 1024) HIPCHK(h, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const uint64_t blocks = (h->n + kBlock - 1) / kBlock;
   void* args[] = {&h->dcfg, &h->dtab, &h->S, (void*)&pdw};
@@ -5216,7 +5489,7 @@ static std::vector<StateSection> state_sections(pgtg_handle* h) {
   add(36, S.occ, (uint64_t)c.nt * 4 * n * 4);
   add(35, S.spawners, (uint64_t)S.sp_pitch * n * 2);
   add(37, S.fresh, (uint64_t)S.fresh_dw * n * 4);
-  add(40, S.qbuf, n * kQueueDepth * (uint64_t)c.qrec_dw * 4);
+  add(40, S.qbuf, n * (uint64_t)queue_depth(h) * (uint64_t)c.qrec_dw * 4);
   add(41, S.qstate, n);
   return v;
 }
@@ -5528,6 +5801,7 @@ const char* pgtg_step_kernel(const pgtg_handle* h) {
   const bool big = h->hcfg.nt > kSmallTiles;
   if (h->hcfg.need_car) return big ? "pgtg::k_env<true, true> + pgtg::k_traffic" : "pgtg::k_env<true, false> + pgtg::k_traffic";
   if (h->hcfg.n_rules > 0) return big ? "pgtg::k_env<true, true>" : "pgtg::k_env<true, false>";
+  if (h->L.queue && h->q_block == 1) return big ? "pgtg::k_envb<true>" : "pgtg::k_envb<false>";
   if (h->L.queue) return big ? "pgtg::k_envq<true>" : "pgtg::k_envq<false>";
   return big ? "pgtg::k_env<false, true>" : "pgtg::k_env<false, false>";
 }

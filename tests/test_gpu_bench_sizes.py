@@ -21,7 +21,7 @@ CASES = {
     "cfg4": (262144, dict(random_map_width=3, random_map_height=3), 30),
     "cfg3": (65536, dict(random_map_width=5, random_map_height=5, traffic_density=0.5), 12),
     # feature variants at multi-workgroup scale (other launch shapes and code paths than the above):
-    # obstacles with every RNG stream, penalties and the cost channel (k_envq with stream resets)
+    # obstacles with every RNG stream, penalties and the cost channel (the map queue with stream resets)
     "obstacles": (32768, dict(random_map_width=4, random_map_height=4, random_map_obstacle_probability=1.0,
                               random_map_ice_probability_weight=1, random_map_broken_road_probability_weight=1,
                               random_map_sand_probability_weight=1, random_map_traffic_light_probability_weight=1,

@@ -226,7 +226,7 @@ def test_rules_added_to_a_ruleless_traffic_handle():
 
 def test_zero_traffic_rule_on_a_handle_without_traffic():
     """A rule with min_traffic = 0 fires without cars: adding it to a no-traffic handle switches the
-    step kernel (k_envq -> k_env<true> with the rules' histogram), removing it switches back."""
+    step kernel (the map queue's k_envb -> k_env<true> with the rules' histogram), removing it switches back."""
     from pgtg_amd.vector import PGTGVecEnv
     rule = {"name": "brake_on_crossings", "tile_type": "1111", "velocity_range": [0.5, 10.0], "min_traffic": 0,
             "min_matching_traffic": 0,
@@ -238,7 +238,7 @@ def test_zero_traffic_rule_on_a_handle_without_traffic():
     cfg.add_rule(with_rule, rule)
     vec = PGTGVecEnv(48, spec=copy.deepcopy(base), device=0)
     try:
-        assert vec.step_kernel() == "pgtg::k_envq<false>"
+        assert vec.step_kernel() == "pgtg::k_envb<false>"
         vec.reset(seed=70)
         vec.add_traffic_rule(rule)
         assert vec.step_kernel() == "pgtg::k_env<true, false>"
@@ -247,7 +247,7 @@ def test_zero_traffic_rule_on_a_handle_without_traffic():
         assert fired > 0
         # back without the rule: the state carries on; compare from a fresh seeded reset
         assert vec.remove_traffic_rule("brake_on_crossings")
-        assert vec.step_kernel() == "pgtg::k_envq<false>"
+        assert vec.step_kernel() == "pgtg::k_envb<false>"
         vec.reset(seed=900)
         _vec_vs_oracle(vec, base, 48, 20, 900, rng, "no rule")
     finally:

@@ -108,6 +108,12 @@ CASES = {
                                             max_allowed_deviation=15, use_sliding_observation_window=True,
                                             use_next_subgoal_direction=True, final_goal_bonus=200,
                                             standing_still_penalty=1), None),
+    # the map-queue step kernels at the shard sizes of 8 and 4 GPUs: k_envb (the automatic choice for
+    # <= 2 rounds of workgroups: rings of three refilled per block) and configs[1] through k_envq's
+    # persistent grid (tune_queue_mode 1)
+    "cfg5_block_131072x40": (131072, 40, dict(random_map_width=5, random_map_height=5), None),
+    "cfg5_block_262144x30": (262144, 30, dict(random_map_width=5, random_map_height=5), None),
+    "cfg2_persistent_4096x100": (4096, 100, dict(random_map_width=3, random_map_height=3), dict(queue_mode=1)),
     "cfg2_wg256_sub32": (4096, 40, dict(random_map_width=3, random_map_height=3),
                          dict(envs_per_block=256, obs_sub=32)),
     "cfg5_wg256": (65536, 20, dict(random_map_width=5, random_map_height=5), dict(envs_per_block=256)),
@@ -130,11 +136,13 @@ def test_every_env_every_step(name):
 
 @pytest.mark.timeout(600)
 def test_one_round_shard_overflow_path():
-    """configs[4]'s per-GPU shard at N = 8 (131 072 envs: one round of map-queue workgroups), every env
-    at every step.  In a one-round launch a workgroup lists at most 64 ring-refill requests; the rest go
-    to the overflow lists that other workgroups' helpers serve in the next launch (pgtg_env.hip k_envq).
+    """configs[4]'s per-GPU shard at N = 8 (131 072 envs: one round of map-queue workgroups) through
+    k_envq's persistent grid (tune_queue_mode 1; the automatic choice there is k_envb, cfg5_block_*),
+    every env at every step.  In a one-round launch a k_envq workgroup lists at most 64 ring-refill
+    requests; the rest go to the overflow lists that other workgroups' helpers serve in the next launch.
     The device counter of overflow requests served shows that this path ran in the compared rollout."""
-    ovf = _compare(_spec(dict(random_map_width=5, random_map_height=5)), 131072, 40, None, "cfg5_all_131072x40")
+    ovf = _compare(_spec(dict(random_map_width=5, random_map_height=5)), 131072, 40, dict(queue_mode=1),
+                   "cfg5_all_131072x40 (k_envq)")
     assert ovf > 0, "no overflow request was served: the one-round overflow path did not run"
 
 

@@ -66,3 +66,46 @@ def test_two_entry_rings_always_hold_the_episode():
             for i, slot, k in served:             # written during the launch, visible after it:
                 assert not (resets[i] and slot == h0[i]), "a refill raced the take of its slot"
                 tag[i, slot] = k
+
+
+def _envb_launch(rng, p, E, spawn, qn, qh, tag, qcap=LANES):
+    """One k_envb launch over one block of E envs (pgtg_env.hip k_envb): the helper refills level 0
+    (empty rings, all of them, before any take) and then levels 1, 2 in list order (env order within a
+    level) up to qcap entries; a reset takes the head; qn/qh follow the kernel's `have` arithmetic."""
+    depth = 3
+    F = [[i for i in range(E) if qn[i] <= l] for l in range(depth)]
+    for i in F[0]:  # heads of empty rings
+        tag[i, qh[i]] = spawn[i]
+    served = [(i, l) for l in range(1, depth) for i in F[l]][:qcap]
+    for i, l in served:  # written by the helper concurrently with the takes of other slots
+        tag[i, (qh[i] + l) % depth] = spawn[i] + 5 * l
+    resets = rng.random(E) < p
+    for i in range(E):
+        have = 1 if qn[i] == 0 else qn[i]
+        have += sum(1 for (j, l) in served if j == i)
+        if resets[i]:
+            assert have >= 1 and tag[i, qh[i]] == spawn[i], "k_envb took an entry not made for its episode"
+            # a refill written in this launch never lands on the slot taken (levels >= 1 are other slots)
+            assert all(l == 0 or (qh[i] + l) % depth != qh[i] for (j, l) in served if j == i)
+            spawn[i] += 5
+            qh[i] = (qh[i] + 1) % depth
+            have -= 1
+        qn[i] = have
+    return resets.sum()
+
+
+def test_three_entry_rings_refilled_per_block():
+    """k_envb: capped refills (64 per launch) with deferral through three-entry rings -- every take is
+    the episode's map, also when a block resets more envs than its helper refills in one launch"""
+    rng = np.random.default_rng(11)
+    for E, p in ((128, 0.43), (128, 1.0), (192, 0.6), (16, 0.43), (64, 0.9)):
+        spawn = np.full(E, 5, np.int64)
+        qn = np.full(E, 3, np.int64)
+        qh = np.zeros(E, np.int64)
+        tag = np.zeros((E, 3), np.int64)
+        for l in range(3):  # k_qfill_b after the reset
+            tag[:, l] = spawn + 5 * l
+        qcap = 2 * LANES if E > 128 else LANES
+        for _t in range(300):
+            _envb_launch(rng, p, E, spawn, qn, qh, tag, qcap)
+            assert (qn >= 0).all() and (qn <= 3).all()
