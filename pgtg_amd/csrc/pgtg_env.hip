@@ -946,7 +946,8 @@ __device__ __forceinline__ void generate_map(const DevCfg& c, const uint32_t* __
 // returns the number of path tiles (0: unreachable).
 // compile_path_m: the same from the interior exit masks (generate_map's `ix`), without the plan reads.
 template <typename M>
-__device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, int s, int g, M hN, M hE, M hS, M hW);
+__device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, int s, int g, M hN, M hE, M hS, M hW,
+                                              uint64_t* dirs = nullptr);
 template <typename M>
 __device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, int s, int g) {
   M hN = mask_zero<M>(), hE = hN, hS = hN, hW = hN;
@@ -964,8 +965,11 @@ __device__ __forceinline__ int compile_path(const DevCfg& c, uint16_t* plan, int
   hW &= mask_h0<M>(c, 3);
   return compile_path_m<M>(c, plan, s, g, hN, hE, hS, hW);
 }
+// dirs (<= 64 tiles): the path tiles per direction N, E, S, W are returned there instead of being
+// marked in the plan (the map queue's entry write folds them into the words it stores)
 template <typename M>
-__device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, int s, int g, M hN, M hE, M hS, M hW) {
+__device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, int s, int g, M hN, M hE, M hS, M hW,
+                                              uint64_t* dirs) {
   const int w = c.tw;
   STAMP(24);
   M vis = mask_bit<M>(g), front = vis;
@@ -998,6 +1002,13 @@ __device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, i
       else { pW |= b; v -= 1; }
       len++;
     }
+    if (dirs) {
+      dirs[0] = (uint64_t)pN;
+      dirs[1] = (uint64_t)pE;
+      dirs[2] = (uint64_t)pS;
+      dirs[3] = (uint64_t)pW;
+      return len;
+    }
     for (M m = pN | pE | pS | pW; m; m &= m - 1) {
       const int t = __builtin_ctzll((uint64_t)m);
       const M b = (M)1 << t;
@@ -1023,12 +1034,15 @@ __device__ __forceinline__ int compile_path_m(const DevCfg& c, uint16_t* plan, i
 
 // The path of a map generate_map<BIG> just built: from its interior exit masks `ix` when it left them
 // (small maps, DevCfg::dual), else from the plan.
+// dirs: as compile_path_m's (maps of <= 64 tiles on the dual path; null otherwise, or the plan is marked)
 template <bool BIG>
-__device__ __forceinline__ int compile_generated(const DevCfg& c, uint16_t* plan, int s, int g, const uint64_t* ix) {
+__device__ __forceinline__ int compile_generated(const DevCfg& c, uint16_t* plan, int s, int g, const uint64_t* ix,
+                                                 uint64_t* dirs = nullptr) {
   if (BIG) return compile_path<Bits<4>>(c, plan, s, g);
   if (c.dual) {
-    if (c.nt <= 32) return compile_path_m<uint32_t>(c, plan, s, g, (uint32_t)ix[0], (uint32_t)ix[1], (uint32_t)ix[2], (uint32_t)ix[3]);
-    return compile_path_m<uint64_t>(c, plan, s, g, ix[0], ix[1], ix[2], ix[3]);
+    if (c.nt <= 32)
+      return compile_path_m<uint32_t>(c, plan, s, g, (uint32_t)ix[0], (uint32_t)ix[1], (uint32_t)ix[2], (uint32_t)ix[3], dirs);
+    return compile_path_m<uint64_t>(c, plan, s, g, ix[0], ix[1], ix[2], ix[3], dirs);
   }
   return c.nt <= 32 ? compile_path<uint32_t>(c, plan, s, g) : compile_path<uint64_t>(c, plan, s, g);
 }
@@ -2739,6 +2753,8 @@ struct Lds {
   int ramp_pct;        // the ramp, in percent of the last launch's first workgroup duration
   int img_in_traf;     // k_env with traffic: the whole workgroup's image in the (after the car pass dead)
                        // traffic region; the agent tile's counters and the reset hand-over words in hist
+  int prio;            // k_envb: issue priority of the env and writer waves over the helper (PGTG_TUNING
+                       // builds only, PGTG_PRIO; 0 otherwise)
   int abl;             // diagnostic ablations (PGTG_TUNING builds only, PGTG_ABL; always 0 otherwise):
                        // k_envq bit 0 no ring refills (the stale entries taken as they are), bit 1 no
                        // terminal-observation writes, bit 2 no observation writes, bit 4 refills without
@@ -2805,8 +2821,10 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
   l.ramp_pct = 25;
   l.img_in_traf = 0;
   l.abl = 0;
+  l.prio = 0;
 #ifdef PGTG_TUNING  // A/B and diagnostic builds only: the product library reads no environment
   if (const char* e = getenv("PGTG_ABL")) l.abl = atoi(e);
+  if (const char* e = getenv("PGTG_PRIO")) l.prio = atoi(e);
   if (const char* e = getenv("PGTG_RAMP")) l.ramp_pct = atoi(e);
   if (const char* e = getenv("PGTG_SPREAD")) l.spread = atoi(e);
   if (const char* e = getenv("PGTG_COMPACT")) l.compact = atoi(e);
@@ -3240,7 +3258,11 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
   int st_t, st_d, gl_t, gl_d;
   uint64_t ix[4];
   generate_map<BIG>(c, BIG ? S.epk : sT.epk, map_rng, plan, st_t, st_d, gl_t, gl_d, ix);
-  int len = compile_generated<BIG>(c, plan, st_t, gl_t, ix);
+  // the path's subgoal directions: kept as four tile masks and folded into the words stored below
+  // (maps of <= 64 tiles on the dual path) instead of a read-modify-write of every path tile's LDS word
+  uint64_t dirs[4] = {0ull, 0ull, 0ull, 0ull};
+  const bool fold = !BIG && c.dual;
+  int len = compile_generated<BIG>(c, plan, st_t, gl_t, ix, fold ? dirs : nullptr);
   int px = 0, py = 0, err = 0;
   if (len <= 0 || !((plan_exits(plan[st_t]) >> st_d) & 1u)) {
     err = len < 0 ? PGTG_E_DEVICE : PGTG_E_MAP;  // (< 0: the path walk's masks were inconsistent)
@@ -3274,6 +3296,15 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
       // tiles >= nt are padding: written as 0 (the scratch holds stale LDS there), so that the queue
       // and the plans taken from it are a function of the seeds alone (byte-identical state dumps)
       wv[j] = (q * 4 + j < pdw) ? (pw[q * 4 + j] & plan_word_mask(c, q * 4 + j)) : 0u;
+      if (fold) {  // direction + 1 into bits 11-13 of both tiles of the word
+        const int t0 = 2 * (q * 4 + j);
+        const uint32_t d0 = (uint32_t)((dirs[0] >> t0) & 1ull) + 2u * (uint32_t)((dirs[1] >> t0) & 1ull) +
+                            3u * (uint32_t)((dirs[2] >> t0) & 1ull) + 4u * (uint32_t)((dirs[3] >> t0) & 1ull);
+        const uint32_t d1 = t0 + 1 < 64 ? (uint32_t)((dirs[0] >> (t0 + 1)) & 1ull) + 2u * (uint32_t)((dirs[1] >> (t0 + 1)) & 1ull) +
+                                          3u * (uint32_t)((dirs[2] >> (t0 + 1)) & 1ull) + 4u * (uint32_t)((dirs[3] >> (t0 + 1)) & 1ull)
+                                        : 0u;
+        wv[j] |= (d0 << 11 | d1 << 27) & plan_word_mask(c, q * 4 + j);
+      }
     }
     d4[q] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
   }
@@ -3719,6 +3750,13 @@ __global__ void __launch_bounds__(kBlock, 4) k_envb(const DevCfg* __restrict__ c
   const uint64_t env0 = (uint64_t)blockIdx.x * L.envs;
   const int nb = (int)min((uint64_t)L.envs, S.n - env0);
   const int env_waves = (L.envs + 63) / 64, gen_wave = env_waves;
+#ifdef PGTG_TUNING
+  if (wave != gen_wave) {  // (A/B) the env and writer waves ahead of the helper in issue arbitration
+    if (L.prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (L.prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (L.prio == 3) __builtin_amdgcn_s_setprio(3);
+  }
+#endif
   // ring entries of levels 1.. regenerated per launch: one per helper lane, two with three env waves
   // (192 envs reset ~80 times per launch at configs[4]'s rate)
   const int qcap = env_waves > 2 ? 2 * kQueueLanes : kQueueLanes;
