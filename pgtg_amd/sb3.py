@@ -169,7 +169,11 @@ class PGTGSB3VecEnv:
         shape, dt = (self.num_envs, self.obs_dim), self._dtype()
         flat = torch.empty(shape, dtype=dt, device=self.venv.device)
         fin = torch.empty(shape, dtype=dt, device=self.venv.device) if final else None
-        self.venv.set_flat_outputs(flat, fin)
+        if getattr(self, "_flat_checked", None) == (dt, final):
+            self.venv._bind_flat_ptrs(flat, fin, 0 if dt == torch.float32 else 1)
+        else:  # (the first binding of this dtype and shape is checked)
+            self.venv.set_flat_outputs(flat, fin)
+            self._flat_checked = (dt, final)
         return flat, fin
 
     def reset(self):
@@ -205,12 +209,18 @@ class PGTGSB3VecEnv:
     def step_wait(self):
         import torch
         kflat = self._kernel_flat()
-        if kflat:
+        if kflat:  # the rows are written by k_flatten in the step: no torch work on the observations
             flat_d, final_d = self._bind_flat(final=True)
-        obs, reward, term, trunc, infos = self.venv.step(self._actions)
+            self.venv.step_launch(self._actions)
+            v = self.venv
+            reward, term, trunc, infos = v.reward, v.terminated, v.truncated, {}
+            if v.cost is not None:
+                infos["cost"] = v.cost
+        else:
+            obs, reward, term, trunc, infos = self.venv.step(self._actions)
         if self.device_obs:
             dones = term | trunc
-            if kflat:  # written by k_flatten in the step: no torch work on the observations
+            if kflat:
                 flat, final = flat_d, final_d
             else:
                 dt = self._dtype()

@@ -91,8 +91,10 @@ class PGTGVecEnv:
     # -- plumbing ------------------------------------------------------------------------------
     def _bind_stream(self):
         import torch
-        s = torch.cuda.current_stream(self.device)
-        _check(self._lib.pgtg_set_stream(self._h, C.c_void_p(s.cuda_stream)), self._h)
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        if s != getattr(self, "_stream", None):  # (a ctypes call only when the stream changed)
+            _check(self._lib.pgtg_set_stream(self._h, C.c_void_p(s)), self._h)
+            self._stream = s
 
     def close(self):
         if getattr(self, "_h", None):
@@ -151,6 +153,19 @@ class PGTGVecEnv:
         return self.observation(), {}
 
     def step(self, actions) -> tuple[dict, Any, Any, Any, dict]:
+        self.step_launch(actions)
+        infos: dict[str, Any] = {"braking_applied": self.braking != 0, "triggered_rules_mask": self.braking}
+        if self.autoreset:
+            done = self.terminated | self.truncated
+            infos["final_observation"] = self.final_observation()
+            infos["_final_observation"] = done
+        if self.cost is not None:
+            infos["cost"] = self.cost
+        return self.observation(), self.reward, self.terminated, self.truncated, infos
+
+    def step_launch(self, actions) -> None:
+        """step() without building the returned dicts: the outputs are in the handle's tensors
+        (obs_map, reward, terminated, truncated, final_map, ..., and any bound flat rows)."""
         import torch
         self._bind_stream()
         if not isinstance(actions, torch.Tensor):
@@ -177,14 +192,6 @@ class PGTGVecEnv:
         _check(self._lib.pgtg_step(self._h, C.c_void_p(a.data_ptr())), self._h)
         if not self.autoreset:
             self._raise_errors()
-        infos: dict[str, Any] = {"braking_applied": self.braking != 0, "triggered_rules_mask": self.braking}
-        if self.autoreset:
-            done = self.terminated | self.truncated
-            infos["final_observation"] = self.final_observation()
-            infos["_final_observation"] = done
-        if self.cost is not None:
-            infos["cost"] = self.cost
-        return self.observation(), self.reward, self.terminated, self.truncated, infos
 
     def step_random(self, seed: int, t: int, env_offset: int = 0):
         """One tick with device-generated uniform random actions (synthetic rollouts, bench)."""
@@ -247,9 +254,14 @@ class PGTGVecEnv:
         if final_flat is not None and not self.autoreset:
             raise ValueError("terminal flat rows need autoreset=True")
         order = flat_order(self.spec)
-        arr = (C.c_int32 * len(order))(*order)
+        self._flat_order = (C.c_int32 * len(order))(*order)
+        self._bind_flat_ptrs(flat, final_flat, 0 if dt == torch.float32 else 1)
+
+    def _bind_flat_ptrs(self, flat, final_flat, dtype_code: int) -> None:
+        """Rebind flat rows already checked by set_flat_outputs (same shape and dtype): the per-step
+        path of PGTGSB3VecEnv, which hands out fresh tensors every step."""
         ptr = lambda x: None if x is None else C.c_void_p(x.data_ptr())  # noqa: E731
-        _check(self._lib.pgtg_set_flat_outputs(self._h, arr, len(order), 0 if dt == torch.float32 else 1,
+        _check(self._lib.pgtg_set_flat_outputs(self._h, self._flat_order, len(self._flat_order), dtype_code,
                                                ptr(flat), ptr(final_flat)), self._h)
         self._flat_refs = (flat, final_flat)  # (the handle writes into them: keep them alive)
 
