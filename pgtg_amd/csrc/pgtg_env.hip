@@ -2748,7 +2748,6 @@ struct Lds {
   int queue;           // step launches use k_envq (maps generated one episode ahead by helper waves)
   int gen_off;         // k_envq: word offset of the helper lanes' plan scratch (kQueueLanes x plan_stride_dw)
   int lm_words;        // terminal-observation line mask words (0: test the selection bytes)
-  int stg_bytes;       // k_envq: the staging wave's block records, ring heads and actions (0: none)
   int stagger;         // first-round start offsets (stagger_start) on
   int stagger_wgs;     // workgroups resident in the first round (blocks per CU x CUs)
   int ramp_pct;        // the ramp, in percent of the last launch's first workgroup duration
@@ -2759,10 +2758,9 @@ struct Lds {
   int abl;             // diagnostic ablations (PGTG_TUNING builds only, PGTG_ABL; always 0 otherwise):
                        // k_envq bit 0 no ring refills (the stale entries taken as they are), bit 1 no
                        // terminal-observation writes, bit 2 no observation writes, bit 4 refills without
-                       // the ring-entry stores, bit 5 no plan-row stores at resets, bit 6 the env waves
-                       // take their own ring heads (the round-5 layout; a valid A/B), bit 7 k_envb writes the
-                       // post-step image of every env as terminal rows (a valid A/B), bit 8 k_envq's env waves
-                       // stage their own blocks (a valid A/B) (timing experiments:
+                       // the ring-entry stores, bit 5 no plan-row stores at resets, bit 7 k_envb writes the
+                       // post-step image of every env as terminal rows (a valid A/B), bit 9 ring entries
+                       // without the folded path directions (marked in LDS; a valid A/B) (timing experiments:
                        // the results are wrong)
 };
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
@@ -2840,16 +2838,13 @@ __host__ inline Lds lds_layout(const DevCfg& c, int envs) {
 // barrier counter) | the terminal-observation line mask (lm_words) | k_envq: the
 // refill lanes' plan scratch (gen_off).  Recomputed whenever the image size changes.
 __host__ inline int tail_bytes(const Lds& l) {
-  return kBlock + (l.queue ? 128 + l.stg_bytes : 32) + 4 * l.lm_words + (l.queue && l.envs <= 32 ? 4 * kViewDw * l.envs : 0);
+  return kBlock + (l.queue ? 128 : 32) + 4 * l.lm_words + (l.queue && l.envs <= 32 ? 4 * kViewDw * l.envs : 0);
 }
 __host__ inline void lds_tail(Lds& l, const DevCfg& c) {
   // line mask: one bit per 128-byte output line of a whole-workgroup image (<= 64 words), else the
   // writers test the per-env selection bytes
   const int64_t total = (int64_t)l.envs * l.seg_bits;
   const int lines = (int)((127 + total) / 128) + 1;
-  // k_envq's staging wave (blocks of 64-128 envs, maps of <= 32 tiles): EnvRec (32 B), ring head and
-  // action per env, 16-byte aligned (it follows the 128-byte counter area)
-  l.stg_bytes = (l.queue && l.envs >= 64 && l.envs <= 128 && c.plan_dq <= 4) ? ((34 * l.envs + 15) & ~15) : 0;
   l.lm_words = (!c.need_car && l.sub_envs >= l.envs && lines <= 64 * 32) ? (lines + 31) / 32 : 0;
 #ifdef PGTG_TUNING
   if (const char* e = getenv("PGTG_LINEMASK")) l.lm_words = atoi(e) ? l.lm_words : 0;
@@ -3258,7 +3253,7 @@ __global__ void __launch_bounds__(kBlock, TR ? 3 : 4) k_env(const DevCfg* __rest
 template <bool BIG>
 __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState& S, uint64_t i, uint32_t k,
                                                 uint16_t* plan, int pdw, uint32_t* __restrict__ dst,
-                                                bool no_store = false) {
+                                                bool no_store = false, bool fold_ok = true) {
   SeedPool sp = ss_pool(S.seed[i]);
   Pcg map_rng = ss_child(sp, k);
   int st_t, st_d, gl_t, gl_d;
@@ -3267,7 +3262,7 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
   // the path's subgoal directions: kept as four tile masks and folded into the words stored below
   // (maps of <= 64 tiles on the dual path) instead of a read-modify-write of every path tile's LDS word
   uint64_t dirs[4] = {0ull, 0ull, 0ull, 0ull};
-  const bool fold = !BIG && c.dual;
+  const bool fold = !BIG && c.dual && fold_ok;
   int len = compile_generated<BIG>(c, plan, st_t, gl_t, ix, fold ? dirs : nullptr);
   int px = 0, py = 0, err = 0;
   if (len <= 0 || !((plan_exits(plan[st_t]) >> st_d) & 1u)) {
@@ -3449,50 +3444,6 @@ __device__ __forceinline__ uint3 ring_take(const DevCfg& c, const DevState& S, c
   return make_uint3(meta.x, meta.y, (meta.z & 0xffffu) | (uint32_t)(-e2) << 16);
 }
 
-// k_envq's staging wave: the record, ring head, action and plan row of envs lane and lane + 64 of a
-// block, loaded into registers (no LDS written yet) ...
-struct Staged {
-  uint4 ra[2], rb[2], pq[2][4];
-  uint32_t qa[2];
-};
-__device__ __forceinline__ Staged stage_issue(const DevCfg& c, const DevState& S, const uint8_t* __restrict__ actions,
-                                              uint64_t env0, int nb, int lane) {
-  Staged g;
-#pragma unroll
-  for (int u = 0; u < 2; u++) {
-    const uint64_t i = env0 + (uint64_t)min(lane + 64 * u, nb - 1);  // (clamped: every load valid)
-    g.ra[u] = S.rec[i].a;
-    g.rb[u] = S.rec[i].b;
-    g.qa[u] = (uint32_t)S.qstate[i] | (uint32_t)actions[i] << 8;
-    const uint4* src = reinterpret_cast<const uint4*>(S.plan + i * (uint64_t)c.plan_stride);
-#pragma unroll
-    for (int q = 0; q < 4; q++) g.pq[u][q] = src[min(q, c.plan_dq - 1)];
-  }
-  return g;
-}
-// ... and written to the block's LDS rows once the previous block no longer reads them
-__device__ __forceinline__ void stage_commit(const Staged& g, uint4* srec, uint8_t* sqa, uint32_t* lds, int pdw, int nb,
-                                             int lane) {
-#pragma unroll
-  for (int u = 0; u < 2; u++) {
-    const int e = lane + 64 * u;
-    if (e < nb) {
-      srec[2 * e] = g.ra[u];
-      srec[2 * e + 1] = g.rb[u];
-      sqa[2 * e] = (uint8_t)g.qa[u];
-      sqa[2 * e + 1] = (uint8_t)(g.qa[u] >> 8);
-      uint32_t* row = lds + e * pdw;
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint32_t wv[4] = {g.pq[u][q].x, g.pq[u][q].y, g.pq[u][q].z, g.pq[u][q].w};
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-          if (q * 4 + j < pdw) row[q * 4 + j] = wv[j];
-      }
-    }
-  }
-}
-
 template <bool BIG>
 __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ cfg, const Tables* __restrict__ gtab,
                                                     DevState S, const uint8_t* __restrict__ actions, PgtgOutputs out,
@@ -3531,8 +3482,8 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   uint32_t* st = lds + L.envs * (pdw + L.scratch_dw + L.traf_dw + L.hist_dw);
   uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
   uint32_t* ctr = reinterpret_cast<uint32_t*>(sel + kBlock);  // sub_barrier counter
-  uint32_t* lm = L.lm_words ? reinterpret_cast<uint32_t*>(sel + kBlock + 128 + L.stg_bytes) : nullptr;  // terminal lines
-  uint32_t* vw = reinterpret_cast<uint32_t*>(sel + kBlock + 128 + L.stg_bytes) + L.lm_words;  // env views (<= 32 envs)
+  uint32_t* lm = L.lm_words ? reinterpret_cast<uint32_t*>(sel + kBlock + 128) : nullptr;  // terminal lines
+  uint32_t* vw = reinterpret_cast<uint32_t*>(sel + kBlock + 128) + L.lm_words;  // env views (<= 32 envs)
   uint32_t* qn = ctr + 1;  // this launch's requests so far
   uint32_t* nxt = ctr + 2;  // the next block
   // blocks after the first: taken from a counter (three, rotating: this launch's, the next one's
@@ -3582,7 +3533,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
           const uint2 r = (uint32_t)lane >= own ? ovf[ob + (lane - own)] : base == 0 ? r0 : req_old[base + lane];
           const uint64_t ie = r.x >> 1;
           gen_queue_entry<BIG>(c, S, ie, r.y, gplan, pdw, S.qbuf + (ie * kQueueDepth + (r.x & 1u)) * (uint64_t)c.qrec_dw,
-                               ABLATE(L, 16));
+                               ABLATE(L, 16), !ABLATE(L, 512));
         }
         if (base + kQueueLanes >= cnt) break;
       }
@@ -3594,7 +3545,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
           const uint2 r = ovf[st0 + lane];
           const uint64_t ie = r.x >> 1;
           gen_queue_entry<BIG>(c, S, ie, r.y, gplan, pdw, S.qbuf + (ie * kQueueDepth + (r.x & 1u)) * (uint64_t)c.qrec_dw,
-                               ABLATE(L, 16));
+                               ABLATE(L, 16), !ABLATE(L, 512));
         }
       }
     }
@@ -3608,22 +3559,6 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
   // ---- env and writer waves (all but the helper), block after block ----
   const int np = kBlock / 64 - 1;  // participating waves
   const int nthr = np * 64;
-  // the last wave (neither env nor helper when a block has <= 128 envs) takes the ring heads
-  const bool taker_on = env_waves <= 2 && !ABLATE(L, 64);
-  // ... and stages the blocks (L.stg_bytes: 64-128 envs, maps of <= 32 tiles): the next block's
-  // records, ring heads, actions and plan rows are loaded while the env waves rebuild this block's
-  // images and written to LDS once they are free, so the env waves start a block without a global load
-  // (whose first use would also wait for the previous block's observation stores: gfx9's vmcnt)
-  const bool stg_on = !BIG && taker_on && L.stg_bytes > 0 && !ABLATE(L, 256);
-  uint4* srec = reinterpret_cast<uint4*>(sel + kBlock + 128);      // [envs][2] EnvRec
-  uint8_t* sqa = reinterpret_cast<uint8_t*>(srec + 2 * L.envs);     // [envs][2] ring head, action
-  const bool stager = stg_on && wave == kBlock / 64 - 1;
-  if (stager) {  // the grid's first block
-    const uint64_t e0 = (uint64_t)blockIdx.x * L.envs;
-    const int n0 = (int)min((uint64_t)L.envs, S.n - e0);
-    const Staged g = stage_issue(c, S, actions, e0, n0, lane);
-    stage_commit(g, srec, sqa, lds, pdw, n0, lane);
-  }
   uint32_t bar = 0;  // running sub_barrier target
   for (uint64_t blk = blockIdx.x; blk < nblk;) {
     STAMP(0);
@@ -3646,7 +3581,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     EnvView v{};
     uint32_t qh = 0;
     int act = 0;
-    if (live && !stg_on) {
+    if (live) {
       v = rec_load(S.rec, i);
       qh = S.qstate[i] & 1u;
       act = actions[i];  // issued with the staging loads, not on the step's chain
@@ -3654,14 +3589,6 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     }
     for (int k = rank; k < L.lm_words; k += nthr) lm[k] = 0u;
     sub_barrier(ctr, bar += (uint32_t)np);  // plans, line mask (and the last block's images written)
-    if (live && stg_on) {  // the staging wave's rows
-      EnvRec r;
-      r.a = srec[2 * slot];
-      r.b = srec[2 * slot + 1];
-      v = rec_view(r);
-      qh = sqa[2 * slot] & 1u;
-      act = sqa[2 * slot + 1];
-    }
     STAMP(1);
     uint8_t my_sel = 0;
     int err = 0;
@@ -3689,118 +3616,108 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
       if (live) write_small_outputs(c, out, i, v, oi, my_sel == 1);
     }
     if (env_wave) sel[slot] = my_sel;
-    if (tid == 0) *nxt = got;  // (read after the next barrier by the staging wave, after the last by all)
-    // the take's hand-over words of a finished env: its spawn counter and ring head in, the entry out
-    uint32_t* xs = lds + L.envs * pdw + (env_wave ? slot : 0) * L.scratch_dw;
-    if (taker_on && my_sel == 1) {
-      xs[0] = v.spawn;
-      xs[1] = qh;
-    }
     const uint64_t rm = __ballot(my_sel == 1);
     if (env_wave && lane == 0 && rm) atomicAdd(&S.counters[1], (unsigned long long)__popcll(rm));
     STAMP(2);
     STAMP(28);
     sub_barrier(ctr, bar += (uint32_t)np);
     STAMP(29);
-    if (taker_on && wave == kBlock / 64 - 1) {
-      // The taker wave loads the finished envs' ring heads while the others write the terminal lines:
-      // the env waves then read their new episodes from LDS.  (A wave's loads are waited for together
-      // with every store it issued before them -- gfx9's vmcnt counts both in order -- so the env waves'
-      // own takes after their terminal stores waited for those stores to drain.)
-      const uint64_t m0 = __ballot(lane < nb && sel[lane] == 1);
-      const uint64_t m1 = __ballot(64 + lane < nb && sel[min(64 + lane, kBlock - 1)] == 1);
-      const int n0 = __popcll(m0), nf = n0 + __popcll(m1);
-      for (int j = lane; j < nf; j += 64) {
-        const int e = j < n0 ? select64(m0, j) : 64 + select64(m1, j - n0);
-        uint32_t* xe = lds + L.envs * pdw + e * L.scratch_dw;
-        const uint3 tk = ring_take<BIG>(c, S, L, env0 + e, xe[1], xe[0], lds + e * pdw, pdw);
-        xe[0] = tk.x;
-        xe[1] = tk.y;
-        xe[2] = tk.z;
-      }
-    } else if (out.final_obs && !ABLATE(L, 2)) {
-      write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, rank,
-                taker_on ? nthr - 64 : nthr, lm);
-    }
+    if (out.final_obs && !ABLATE(L, 2))
+      write_obs(out.final_obs + env0 * (uint64_t)c.obs_bytes, (uint32_t)nb, (uint32_t)c.obs_bytes, st, sel, rank, nthr, lm);
     STAMP(3);
-    sub_barrier(ctr, bar += (uint32_t)np);  // terminal images written before they are rebuilt (and the takes in)
-    if (stager) {
-      // the staging wave (no env slots, no part in the images of blocks of >= 64 envs): the next block's
-      // rows, loaded while the env waves rebuild this block's images, written once they are done with
-      // this block's plan rows -- its own path, so that the loaded registers are not held across theirs
-      const uint32_t gn = *nxt;
-      // (the block counter runs past the last block: a value at or beyond it ends the loop, nothing to stage)
-      if (gn != 0xffffffffu && (uint64_t)gridDim.x + gn < nblk) {
-        const uint64_t nenv0 = ((uint64_t)gridDim.x + gn) * (uint64_t)L.envs;
-        const int nnb = (int)min((uint64_t)L.envs, S.n - nenv0);
-        const Staged stg = stage_issue(c, S, actions, nenv0, nnb, lane);
-        sub_barrier(ctr, bar += (uint32_t)np);
-        stage_commit(stg, srec, sqa, lds, pdw, nnb, lane);
-      } else {
-        sub_barrier(ctr, bar += (uint32_t)np);
-      }
-    } else {
-      const bool reset_now = my_sel != 0;
-      const uint32_t k0 = v.spawn;
-      if (reset_now) {  // the ring's head becomes the episode (env_reset without the generation)
-        const uint3 tk = taker_on ? make_uint3(xs[0], xs[1], xs[2]) : ring_take<BIG>(c, S, L, i, qh, k0, plan_w, pdw);
-        v.spawn = k0 + 5u;
-        v.sg = tk.y;
-        v.used = 0;
-        v.path_len = tk.z & 0xffffu;
-        v.flags = 0;
-        v.phase = 0;
-        v.elapsed = 0;
-        v.vx = v.vy = 0;
-        v.px = (int)(int16_t)(tk.x & 0xffffu);
-        v.py = (int)(int16_t)(tk.x >> 16);
-        const int e2 = -(int)(tk.z >> 16);
-        if (e2) err = e2;
-        if (S.visited && e2 == 0) {
-          uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
-          for (int q2 = 0; q2 < c.vis_words; q2++) vis[q2] = 0;
-          int b = (v.px + 2) * c.vis_pitch + (v.py + 2);
-          vis[b >> 5] |= 1u << (b & 31);
+    sub_barrier(ctr, bar += (uint32_t)np);  // terminal images written before they are rebuilt
+    const bool reset_now = my_sel != 0;
+    const uint32_t k0 = v.spawn;
+    if (reset_now) {  // the ring's head becomes the episode (env_reset without the generation)
+      const uint4* q4 = reinterpret_cast<const uint4*>(S.qbuf + (i * kQueueDepth + qh) * (uint64_t)c.qrec_dw);
+      uint4* dstp = reinterpret_cast<uint4*>(S.plan + i * (uint64_t)c.plan_stride);
+      // all loads of the entry first: a load after a store to S.plan (which the compiler cannot
+      // tell apart from the queue) would wait for the one before it, one HBM latency per 16 bytes
+      const int nq = c.plan_dq;  // 16-byte words of the tile plan (<= 8 unless BIG)
+      const uint4 meta = q4[nq];
+      for (int k0q = 0; k0q < (BIG ? nq : 1); k0q += 8) {
+        uint4 qw[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) qw[k] = q4[k0q + k < nq ? k0q + k : k0q];  // unconditional: registers, not scratch
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          if (k0q + k < nq) {
+            if (!ABLATE(L, 32)) dstp[k0q + k] = qw[k];
+            const uint32_t wv[4] = {qw[k].x, qw[k].y, qw[k].z, qw[k].w};
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              if ((k0q + k) * 4 + j < pdw) plan_w[(k0q + k) * 4 + j] = wv[j];
+          }
         }
       }
-      STAMP(4);
-      // refill request: the next-but-one episode's map (spawn counter k0 + 10) into the slot just taken
-      const uint64_t rb = __ballot(reset_now);
-      if (rb) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(qn, (uint32_t)__popcll(rb));
-        base = __builtin_amdgcn_readfirstlane(base);
-        const uint32_t k = (uint32_t)__popcll(rb);
-        // one round: list positions >= kQueueLanes go to the overflow list
-        const uint32_t ovn = (one_round && base + k > (uint32_t)kQueueLanes) ? base + k - max(base, (uint32_t)kQueueLanes) : 0u;
-        uint32_t obase = 0;
-        if (ovn) {
-          if (lane == 0) obase = atomicAdd(&S.qctr[kQctrOvfLen + set_new * 8u + ox], ovn);
-          obase = __builtin_amdgcn_readfirstlane(obase);
-        }
-        if (reset_now) {
-          const uint32_t p = base + (uint32_t)__popcll(rb & ((1ull << lane) - 1ull));
-          const uint2 r = make_uint2((uint32_t)i << 1 | qh, k0 + 10u);
-          if (one_round && p >= (uint32_t)kQueueLanes)
-            S.qovf[((uint64_t)par * 8u + ox) * ocap + obase + (p - max(base, (uint32_t)kQueueLanes))] = r;
-          else
-            req_new[p] = r;
-          S.qstate[i] = (uint8_t)(qh ^ 1u);  // (every env's byte instead: 403.3 vs 401.4 us)
-        }
+      if (!ABLATE(L, 32))
+        for (int k = nq; k < c.plan_stride / 8; k++) dstp[k] = make_uint4(0u, 0u, 0u, 0u);  // the row's whole lines
+      if (c.need_ice || c.need_broken || c.need_sand) {
+        SeedPool sp = ss_pool(S.seed[i]);
+        if (c.need_ice) stream_store_all(S.ice, i, ss_child(sp, k0 + 2u));
+        if (c.need_broken) stream_store_all(S.broken, i, ss_child(sp, k0 + 3u));
+        if (c.need_sand) stream_store_all(S.sand, i, ss_child(sp, k0 + 4u));
       }
-      if (live) {
-        rec_store(S.rec, i, v);
-        S.err[i] = (uint8_t)(-err);
+      v.spawn = k0 + 5u;
+      v.sg = meta.y;
+      v.used = 0;
+      v.path_len = meta.z & 0xffffu;
+      v.flags = 0;
+      v.phase = 0;
+      v.elapsed = 0;
+      v.vx = v.vy = 0;
+      v.px = (int)(int16_t)(meta.x & 0xffffu);
+      v.py = (int)(int16_t)(meta.x >> 16);
+      // the entry was generated for this episode (spawn counter k0): every launch serves all of the
+      // previous launch's requests and the ring holds two entries, so it always is -- a mismatch is
+      // reported as a device error, never used
+      const int e2 = (meta.w != queue_tag(k0) && !ABLATE(L, 1 | 16)) ? PGTG_E_DEVICE : -(int)(meta.z >> 16);
+      if (e2) err = e2;
+      if (S.visited && e2 == 0) {
+        uint32_t* vis = S.visited + i * (uint64_t)c.vis_words;
+        for (int q2 = 0; q2 < c.vis_words; q2++) vis[q2] = 0;
+        int b = (v.px + 2) * c.vis_pitch + (v.py + 2);
+        vis[b >> 5] |= 1u << (b & 31);
       }
-      STAMP(5);
-      {
-        ObsInfo oi;
-        group_obs<BIG>(c, S, v, reset_now, st, oi, L, wave, lane, ctr, bar, np, rank, vw, false);
-        if (reset_now) write_small_outputs(c, out, i, v, oi, false);
-      }
-      STAMP(30);
-      sub_barrier(ctr, bar += (uint32_t)np);
     }
+    STAMP(4);
+    // refill request: the next-but-one episode's map (spawn counter k0 + 10) into the slot just taken
+    const uint64_t rb = __ballot(reset_now);
+    if (rb) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(qn, (uint32_t)__popcll(rb));
+      base = __builtin_amdgcn_readfirstlane(base);
+      const uint32_t k = (uint32_t)__popcll(rb);
+      // one round: list positions >= kQueueLanes go to the overflow list
+      const uint32_t ovn = (one_round && base + k > (uint32_t)kQueueLanes) ? base + k - max(base, (uint32_t)kQueueLanes) : 0u;
+      uint32_t obase = 0;
+      if (ovn) {
+        if (lane == 0) obase = atomicAdd(&S.qctr[kQctrOvfLen + set_new * 8u + ox], ovn);
+        obase = __builtin_amdgcn_readfirstlane(obase);
+      }
+      if (reset_now) {
+        const uint32_t p = base + (uint32_t)__popcll(rb & ((1ull << lane) - 1ull));
+        const uint2 r = make_uint2((uint32_t)i << 1 | qh, k0 + 10u);
+        if (one_round && p >= (uint32_t)kQueueLanes)
+          S.qovf[((uint64_t)par * 8u + ox) * ocap + obase + (p - max(base, (uint32_t)kQueueLanes))] = r;
+        else
+          req_new[p] = r;
+        S.qstate[i] = (uint8_t)(qh ^ 1u);  // (every env's byte instead: 403.3 vs 401.4 us)
+      }
+    }
+    if (live) {
+      rec_store(S.rec, i, v);
+      S.err[i] = (uint8_t)(-err);
+    }
+    STAMP(5);
+    {
+      ObsInfo oi;
+      group_obs<BIG>(c, S, v, reset_now, st, oi, L, wave, lane, ctr, bar, np, rank, vw, false);
+      if (reset_now) write_small_outputs(c, out, i, v, oi, false);
+    }
+    if (tid == 0) *nxt = got;
+    STAMP(30);
+    sub_barrier(ctr, bar += (uint32_t)np);
     STAMP(31);
     if (tid == 0)  // (every request of the block is in)
       S.qctr[par * gridDim.x + blockIdx.x] = one_round ? min(*qn, (uint32_t)kQueueLanes) : *qn;
@@ -3811,8 +3728,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
     if (blk == blockIdx.x) stagger_record(L, S, t_start);
     STAMP(6);
     blk = g == 0xffffffffu ? nblk : (uint64_t)gridDim.x + g;
-  }
-  STAMPR(3);
+  }  STAMPR(3);
 }
 
 // Step launch with the map queue for grids of at most two rounds of workgroups (k_envb: the map
@@ -3860,8 +3776,8 @@ __global__ void __launch_bounds__(kBlock, 4) k_envb(const DevCfg* __restrict__ c
   uint8_t* sel = reinterpret_cast<uint8_t*>(st + L.stream_words);  // [kBlock]
   uint64_t* fm = reinterpret_cast<uint64_t*>(sel + kBlock);  // [level][env wave]: envs refilled at ring level
   uint32_t* ctr = reinterpret_cast<uint32_t*>(fm + 3 * kBlockDepth);  // sub_barrier counter
-  uint32_t* lm = L.lm_words ? reinterpret_cast<uint32_t*>(sel + kBlock + 128 + L.stg_bytes) : nullptr;  // terminal lines
-  uint32_t* vw = reinterpret_cast<uint32_t*>(sel + kBlock + 128 + L.stg_bytes) + L.lm_words;  // env views (<= 32 envs)
+  uint32_t* lm = L.lm_words ? reinterpret_cast<uint32_t*>(sel + kBlock + 128) : nullptr;  // terminal lines
+  uint32_t* vw = reinterpret_cast<uint32_t*>(sel + kBlock + 128) + L.lm_words;  // env views (<= 32 envs)
   Plan pl{reinterpret_cast<uint16_t*>(plan_w)};
 
   EnvView v{};
@@ -3916,7 +3832,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envb(const DevCfg* __restrict__ c
       const uint32_t qe = xf[e * L.scratch_dw + 1];
       const uint32_t rslot = (((qe >> 2) & 3u) + (uint32_t)l) % (uint32_t)kBlockDepth;
       gen_queue_entry<BIG>(c, S, ie, xf[e * L.scratch_dw] + 5u * (uint32_t)l, gplan, pdw,
-                      S.qbuf + (ie * kBlockDepth + rslot) * (uint64_t)c.qrec_dw, ABLATE(L, 16));
+                      S.qbuf + (ie * kBlockDepth + rslot) * (uint64_t)c.qrec_dw, ABLATE(L, 16), !ABLATE(L, 512));
     };
     if (ABLATE(L, 1)) {
       if (any_empty) __syncthreads();
@@ -4414,37 +4330,6 @@ __global__ void __launch_bounds__(256) k_flatten(FlatArgs a) {
 #pragma unroll
     for (int u = 0; u < G; u++)
       if (keep[u]) d[u] = v[u];
-  }
-}
-
-// The terminal rows: few envs finish per step (configs with TimeLimit(100): ~1-2 %), so a workgroup
-// takes 256 envs, lists the finished ones in LDS and writes their rows together (256 consecutive
-// values per pass), instead of a thread per 16 output bytes of every row testing its env's flags.
-template <typename T>
-__global__ void __launch_bounds__(256) k_flatten_final(FlatArgs a) {
-  __shared__ uint32_t list[256];
-  __shared__ uint32_t cnt;
-  const uint64_t e0 = (uint64_t)blockIdx.x * 256;
-  if (threadIdx.x == 0) cnt = 0u;
-  __syncthreads();
-  const uint64_t e = e0 + threadIdx.x;
-  const bool done = e < a.n && (a.term[e] | a.trunc[e]);
-  const uint64_t m = __ballot(done);
-  if (m) {  // one LDS atomic per wave, the wave's finished envs in lane order
-    uint32_t base = 0;
-    if ((threadIdx.x & 63) == 0) base = atomicAdd(&cnt, (uint32_t)__popcll(m));
-    base = __shfl(base, 0);
-    if (done) list[base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1ull))] = threadIdx.x;
-  }
-  __syncthreads();
-  const uint32_t nd = cnt;
-  for (uint32_t k = 0; k < nd; k++) {
-    const uint64_t ee = e0 + list[k];
-    T* row = reinterpret_cast<T*>(a.dst) + ee * (uint64_t)a.D;
-    for (uint32_t j = threadIdx.x; j < (uint32_t)a.D; j += 256) {
-      const uint32_t slot = j < (uint32_t)a.cw2 ? j / (uint32_t)a.w2 : 0u;
-      row[j] = flat_value<T>(a, ee, j, slot, j - slot * (uint32_t)a.w2);
-    }
   }
 }
 
@@ -5232,13 +5117,9 @@ static int launch_flatten(pgtg_handle* h, bool final) {
   a.trunc = o.truncated;
   a.dst = final ? h->final_flat_dst : h->flat_dst;
   a.final = final ? 1 : 0;
-  if (final) {  // (the finished envs' rows only)
-    const dim3 grid((unsigned)((h->n + 255) / 256));
-    if (h->flat_dtype) hipLaunchKernelGGL(k_flatten_final<int8_t>, grid, dim3(256), 0, h->stream, a);
-    else hipLaunchKernelGGL(k_flatten_final<float>, grid, dim3(256), 0, h->stream, a);
-    HIPCHK(h, hipGetLastError());
-    return PGTG_OK;
-  }
+  // (the terminal rows by the same grid, every thread testing its rows' flags: a workgroup per 256 envs
+  // writing its finished envs' rows together measured slower -- its rows' loads were one chain --
+  // adapter 70.7 vs 57.2 M env-steps/s, profiles/r06/s5)
   const uint64_t chunks = (h->n * (uint64_t)a.D * (h->flat_dtype ? 1u : 4u) + 15) / 16;
   const dim3 grid((unsigned)((chunks + 255) / 256));
   if (h->flat_dtype) hipLaunchKernelGGL(k_flatten<int8_t>, grid, dim3(256), 0, h->stream, a);
