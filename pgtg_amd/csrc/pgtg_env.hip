@@ -2759,8 +2759,8 @@ struct Lds {
                        // k_envq bit 0 no ring refills (the stale entries taken as they are), bit 1 no
                        // terminal-observation writes, bit 2 no observation writes, bit 4 refills without
                        // the ring-entry stores, bit 5 no plan-row stores at resets, bit 7 k_envb writes the
-                       // post-step image of every env as terminal rows (a valid A/B), bit 9 ring entries
-                       // without the folded path directions (marked in LDS; a valid A/B) (timing experiments:
+                       // post-step image of every env as terminal rows (a valid A/B), bit 9 k_envb's ring
+                       // entries without the folded path directions (marked in LDS; a valid A/B) (timing experiments:
                        // the results are wrong)
 };
 constexpr int kQueueLanes = 64;  // k_envq lanes that generate queued maps (one wave)
@@ -3260,7 +3260,10 @@ __device__ __forceinline__ void gen_queue_entry(const DevCfg& c, const DevState&
   uint64_t ix[4];
   generate_map<BIG>(c, BIG ? S.epk : sT.epk, map_rng, plan, st_t, st_d, gl_t, gl_d, ix);
   // the path's subgoal directions: kept as four tile masks and folded into the words stored below
-  // (maps of <= 64 tiles on the dual path) instead of a read-modify-write of every path tile's LDS word
+  // (maps of <= 64 tiles on the dual path) instead of a read-modify-write of every path tile's LDS word.
+  // k_envb folds (one-round launches, where the helper's chain counts: 131 072 envs 70.4 vs 71.2 us),
+  // k_envq does not (eight rounds, where the helpers' instructions count against the env waves' issue:
+  // 1 048 576 envs 400 vs 406.7 us; profiles/r06/s8); k_qfill's entries are the same either way
   uint64_t dirs[4] = {0ull, 0ull, 0ull, 0ull};
   const bool fold = !BIG && c.dual && fold_ok;
   int len = compile_generated<BIG>(c, plan, st_t, gl_t, ix, fold ? dirs : nullptr);
@@ -3533,7 +3536,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
           const uint2 r = (uint32_t)lane >= own ? ovf[ob + (lane - own)] : base == 0 ? r0 : req_old[base + lane];
           const uint64_t ie = r.x >> 1;
           gen_queue_entry<BIG>(c, S, ie, r.y, gplan, pdw, S.qbuf + (ie * kQueueDepth + (r.x & 1u)) * (uint64_t)c.qrec_dw,
-                               ABLATE(L, 16), !ABLATE(L, 512));
+                               ABLATE(L, 16), false);
         }
         if (base + kQueueLanes >= cnt) break;
       }
@@ -3545,7 +3548,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_envq(const DevCfg* __restrict__ c
           const uint2 r = ovf[st0 + lane];
           const uint64_t ie = r.x >> 1;
           gen_queue_entry<BIG>(c, S, ie, r.y, gplan, pdw, S.qbuf + (ie * kQueueDepth + (r.x & 1u)) * (uint64_t)c.qrec_dw,
-                               ABLATE(L, 16), !ABLATE(L, 512));
+                               ABLATE(L, 16), false);
         }
       }
     }
@@ -4281,55 +4284,68 @@ struct FlatArgs {
   int32_t D, OB, w2, cw2, nsd_on, final;
   uint8_t order[PGTG_MAX_CHANNELS];  // channel (in the observation) of the k-th name-sorted key
 };
+// One workgroup takes the rows b, b + G, b + 2G, ... of the grid's G workgroups (at most 256): it lists
+// the rows to write (every row, or the finished envs' for the terminal rows) and writes them one after
+// the other, each row's values by its 256 threads with every load of the row issued before the first
+// store (a row of up to 8 x 256 values in one pass).  A thread per 16 output bytes of the whole array,
+// the first version, spent its time in a 64-bit division and in launching 18 M threads, most of which
+// had nothing to do on the terminal pass (166 us per pass at 65 536 envs, profiles/r06/s8).
 template <typename T>
-__device__ __forceinline__ T flat_value(const FlatArgs& a, uint64_t e, uint32_t j, uint32_t slot, uint32_t sq) {
-  if (j < (uint32_t)a.cw2) return (T)a.obs[e * (uint64_t)a.OB + (uint32_t)a.order[slot] * (uint32_t)a.w2 + sq];
-  int k = (int)(j - (uint32_t)a.cw2);
+__device__ __forceinline__ T flat_tail(const FlatArgs& a, int k, int nsdv, int px, int py, int vx, int vy) {
   if (a.nsd_on) {
-    if (k < 9) return (T)(k == a.nsd[e] + 1 ? 1 : 0);
+    if (k < 9) return (T)(k == nsdv ? 1 : 0);
     k -= 9;
   }
-  if (k < 9) return (T)(k == a.pos[2 * e] ? 1 : 0);
-  if (k < 18) return (T)(k - 9 == a.pos[2 * e + 1] ? 1 : 0);
-  return (T)a.vel[2 * e + (k - 18)];
+  if (k < 9) return (T)(k == px ? 1 : 0);
+  if (k < 18) return (T)(k - 9 == py ? 1 : 0);
+  return (T)(k == 18 ? vx : vy);
 }
 template <typename T>
 __global__ void __launch_bounds__(256) k_flatten(FlatArgs a) {
-  constexpr int G = 16 / sizeof(T);
-  const uint64_t total = a.n * (uint64_t)a.D;
-  const uint64_t g0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * G;
-  if (g0 >= total) return;
-  uint64_t e = g0 / (uint64_t)a.D;
-  uint32_t j = (uint32_t)(g0 - e * (uint64_t)a.D);
-  uint32_t slot = j < (uint32_t)a.cw2 ? j / (uint32_t)a.w2 : 0u, sq = j < (uint32_t)a.cw2 ? j - slot * (uint32_t)a.w2 : 0u;
-  bool keep0 = !a.final || (a.term[e] | a.trunc[e]);
-  T v[G];
-  bool keep[G];
-#pragma unroll
-  for (int u = 0; u < G; u++) {
-    keep[u] = g0 + u < total && keep0;
-    v[u] = keep[u] ? flat_value<T>(a, e, j, slot, sq) : (T)0;
-    // next element: the next square / channel / tail value, or the next env's row
-    if (++j == (uint32_t)a.D) {
-      j = slot = sq = 0u;
-      if (++e < a.n) keep0 = !a.final || (a.term[e] | a.trunc[e]);
-    } else if (++sq == (uint32_t)a.w2) {
-      sq = 0u;
-      slot++;
-    }
+  __shared__ uint32_t choff[PGTG_MAX_CHANNELS];  // byte offset in the obs row of the k-th name-sorted channel
+  __shared__ uint32_t rows[256];
+  __shared__ uint32_t nrows;
+  const int t = threadIdx.x;
+  const uint32_t D = (uint32_t)a.D, w2 = (uint32_t)a.w2, cw2 = (uint32_t)a.cw2;
+  for (uint32_t k = t; k * w2 < cw2; k += 256) choff[k] = (uint32_t)a.order[k] * w2;
+  if (t == 0) nrows = 0u;
+  __syncthreads();
+  const uint64_t e = blockIdx.x + (uint64_t)t * gridDim.x;
+  bool keep = e < a.n;
+  if (keep && a.final) keep = (a.term[e] | a.trunc[e]) != 0;
+  const uint64_t m = __ballot(keep);
+  if (m) {
+    uint32_t base = 0;
+    if ((t & 63) == 0) base = atomicAdd(&nrows, (uint32_t)__popcll(m));
+    base = __shfl(base, 0);
+    if (keep) rows[base + __popcll(m & ((1ull << (t & 63)) - 1ull))] = (uint32_t)t;
   }
-  T* d = reinterpret_cast<T*>(a.dst) + g0;
-  bool all = true;
+  __syncthreads();
+  const uint32_t nr = nrows;
+  for (uint32_t r = 0; r < nr; r++) {
+    const uint64_t er = blockIdx.x + (uint64_t)rows[r] * gridDim.x;
+    const uint8_t* __restrict__ orow = a.obs + er * (uint64_t)a.OB;
+    T* __restrict__ row = reinterpret_cast<T*>(a.dst) + er * (uint64_t)D;
+    const int nsdv = a.nsd_on ? a.nsd[er] + 1 : -1;
+    const int px = a.pos[2 * er], py = a.pos[2 * er + 1], vx = a.vel[2 * er], vy = a.vel[2 * er + 1];
+    constexpr int U = 8;
+    T v[U];
 #pragma unroll
-  for (int u = 0; u < G; u++) all = all && keep[u];
-  if (all) {
-    uint4 q;
-    __builtin_memcpy(&q, v, 16);
-    *reinterpret_cast<uint4*>(d) = q;
-  } else {
+    for (int u = 0; u < U; u++) {
+      const uint32_t j = (uint32_t)t + (uint32_t)u * 256u;
+      const uint32_t slot = j < cw2 ? j / w2 : 0u;
+      const uint8_t ob = orow[j < cw2 ? choff[slot] + (j - slot * w2) : 0u];  // (unconditional: one batch of loads)
+      v[u] = j < cw2 ? (T)ob : flat_tail<T>(a, (int)(j - cw2), nsdv, px, py, vx, vy);
+    }
 #pragma unroll
-    for (int u = 0; u < G; u++)
-      if (keep[u]) d[u] = v[u];
+    for (int u = 0; u < U; u++) {
+      const uint32_t j = (uint32_t)t + (uint32_t)u * 256u;
+      if (j < D) row[j] = v[u];
+    }
+    for (uint32_t j = (uint32_t)t + U * 256u; j < D; j += 256u) {  // (rows of more than 2 048 values)
+      const uint32_t slot = j < cw2 ? j / w2 : 0u;
+      row[j] = j < cw2 ? (T)orow[choff[slot] + (j - slot * w2)] : flat_tail<T>(a, (int)(j - cw2), nsdv, px, py, vx, vy);
+    }
   }
 }
 
@@ -5117,13 +5133,10 @@ static int launch_flatten(pgtg_handle* h, bool final) {
   a.trunc = o.truncated;
   a.dst = final ? h->final_flat_dst : h->flat_dst;
   a.final = final ? 1 : 0;
-  // (the terminal rows by the same grid, every thread testing its rows' flags: a workgroup per 256 envs
-  // writing its finished envs' rows together measured slower -- its rows' loads were one chain --
-  // adapter 70.7 vs 57.2 M env-steps/s, profiles/r06/s5)
-  const uint64_t chunks = (h->n * (uint64_t)a.D * (h->flat_dtype ? 1u : 4u) + 15) / 16;
-  const dim3 grid((unsigned)((chunks + 255) / 256));
-  if (h->flat_dtype) hipLaunchKernelGGL(k_flatten<int8_t>, grid, dim3(256), 0, h->stream, a);
-  else hipLaunchKernelGGL(k_flatten<float>, grid, dim3(256), 0, h->stream, a);
+  // rows per workgroup <= 256; a grid of >= 2 048 workgroups where the batch allows
+  const uint64_t G = std::max<uint64_t>(std::min<uint64_t>(h->n, 2048), (h->n + 255) / 256);
+  if (h->flat_dtype) hipLaunchKernelGGL(k_flatten<int8_t>, dim3((unsigned)G), dim3(256), 0, h->stream, a);
+  else hipLaunchKernelGGL(k_flatten<float>, dim3((unsigned)G), dim3(256), 0, h->stream, a);
   HIPCHK(h, hipGetLastError());
   return PGTG_OK;
 }
