@@ -4285,9 +4285,8 @@ struct FlatArgs {
   uint8_t order[PGTG_MAX_CHANNELS];  // channel (in the observation) of the k-th name-sorted key
 };
 // One workgroup takes the rows b, b + G, b + 2G, ... of the grid's G workgroups (at most 256): it lists
-// the rows to write (every row, or the finished envs' for the terminal rows) and writes them one after
-// the other, each row's values by its 256 threads with every load of the row issued before the first
-// store (a row of up to 8 x 256 values in one pass).  A thread per 16 output bytes of the whole array,
+// the rows to write (every row, or the finished envs' for the terminal rows) and its waves write them,
+// a row per wave.  A thread per 16 output bytes of the whole array,
 // the first version, spent its time in a 64-bit division and in launching 18 M threads, most of which
 // had nothing to do on the terminal pass (166 us per pass at 65 536 envs, profiles/r06/s8).
 template <typename T>
@@ -4300,14 +4299,32 @@ __device__ __forceinline__ T flat_tail(const FlatArgs& a, int k, int nsdv, int p
   if (k < 18) return (T)(k - 9 == py ? 1 : 0);
   return (T)(k == 18 ? vx : vy);
 }
+constexpr int kFlatU = 18;  // values per lane in one pass of a row: rows of up to 18 x 64 = 1 152 in one pass
+// V consecutive values per lane and store (V = 2: float pairs, rows of an even D are 8-byte aligned)
+template <typename T, int V>
+struct FlatVec;
+template <>
+struct FlatVec<float, 2> {
+  using type = float2;
+  __device__ static float2 make(const float* f) { return make_float2(f[0], f[1]); }
+};
 template <typename T>
+struct FlatVec<T, 1> {
+  using type = T;
+  __device__ static T make(const T* f) { return f[0]; }
+};
+template <typename T, int V>
 __global__ void __launch_bounds__(256) k_flatten(FlatArgs a) {
-  __shared__ uint32_t choff[PGTG_MAX_CHANNELS];  // byte offset in the obs row of the k-th name-sorted channel
+  // obs byte offset of the row's first kFlatU x 64 values (channels in name order), built once
+  __shared__ uint32_t offs[kFlatU * 64];
   __shared__ uint32_t rows[256];
   __shared__ uint32_t nrows;
   const int t = threadIdx.x;
   const uint32_t D = (uint32_t)a.D, w2 = (uint32_t)a.w2, cw2 = (uint32_t)a.cw2;
-  for (uint32_t k = t; k * w2 < cw2; k += 256) choff[k] = (uint32_t)a.order[k] * w2;
+  for (uint32_t j = t; j < (uint32_t)(kFlatU * 64); j += 256) {
+    const uint32_t slot = j < cw2 ? j / w2 : 0u;
+    offs[j] = j < cw2 ? (uint32_t)a.order[slot] * w2 + (j - slot * w2) : 0u;
+  }
   if (t == 0) nrows = 0u;
   __syncthreads();
   const uint64_t e = blockIdx.x + (uint64_t)t * gridDim.x;
@@ -4322,29 +4339,36 @@ __global__ void __launch_bounds__(256) k_flatten(FlatArgs a) {
   }
   __syncthreads();
   const uint32_t nr = nrows;
-  for (uint32_t r = 0; r < nr; r++) {
+  // one row per wave at a time (the workgroup's four waves on four rows): every load of a pass -- the
+  // observation bytes and the tail's scalars -- issued before its first store, so a row of <= 1 152
+  // values costs one memory round trip; lane l writes values V(l + 64k) .. V(l + 64k) + V - 1
+  constexpr int P = kFlatU / V;  // stores per lane and pass
+  using VT = typename FlatVec<T, V>::type;
+  const int wv = t >> 6, ln = t & 63;
+  for (uint32_t r = (uint32_t)wv; r < nr; r += 4u) {
     const uint64_t er = blockIdx.x + (uint64_t)rows[r] * gridDim.x;
     const uint8_t* __restrict__ orow = a.obs + er * (uint64_t)a.OB;
     T* __restrict__ row = reinterpret_cast<T*>(a.dst) + er * (uint64_t)D;
     const int nsdv = a.nsd_on ? a.nsd[er] + 1 : -1;
     const int px = a.pos[2 * er], py = a.pos[2 * er + 1], vx = a.vel[2 * er], vy = a.vel[2 * er + 1];
-    constexpr int U = 8;
-    T v[U];
+    for (uint32_t j0 = 0; j0 < D; j0 += kFlatU * 64u) {
+      uint32_t ob[kFlatU];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t j = (uint32_t)t + (uint32_t)u * 256u;
-      const uint32_t slot = j < cw2 ? j / w2 : 0u;
-      const uint8_t ob = orow[j < cw2 ? choff[slot] + (j - slot * w2) : 0u];  // (unconditional: one batch of loads)
-      v[u] = j < cw2 ? (T)ob : flat_tail<T>(a, (int)(j - cw2), nsdv, px, py, vx, vy);
-    }
+      for (int u = 0; u < kFlatU; u++) {
+        const uint32_t j = j0 + (uint32_t)V * ((uint32_t)ln + (uint32_t)(u / V) * 64u) + (uint32_t)(u % V);
+        const uint32_t jj = j - j0;  // (< kFlatU x 64)
+        const uint32_t off = j0 == 0 ? offs[jj] : (j < cw2 ? (uint32_t)a.order[j / w2] * w2 + j % w2 : 0u);
+        ob[u] = orow[j < cw2 ? off : 0u];  // (unconditional: one batch of loads)
+      }
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t j = (uint32_t)t + (uint32_t)u * 256u;
-      if (j < D) row[j] = v[u];
-    }
-    for (uint32_t j = (uint32_t)t + U * 256u; j < D; j += 256u) {  // (rows of more than 2 048 values)
-      const uint32_t slot = j < cw2 ? j / w2 : 0u;
-      row[j] = j < cw2 ? (T)orow[choff[slot] + (j - slot * w2)] : flat_tail<T>(a, (int)(j - cw2), nsdv, px, py, vx, vy);
+      for (int p = 0; p < P; p++) {
+        const uint32_t j = j0 + (uint32_t)V * ((uint32_t)ln + (uint32_t)p * 64u);
+        T f[V];
+#pragma unroll
+        for (int h = 0; h < V; h++)
+          f[h] = j + h < cw2 ? (T)ob[p * V + h] : flat_tail<T>(a, (int)(j + h - cw2), nsdv, px, py, vx, vy);
+        if (j < D) *reinterpret_cast<VT*>(row + j) = FlatVec<T, V>::make(f);  // (D % V == 0)
+      }
     }
   }
 }
@@ -5133,10 +5157,11 @@ static int launch_flatten(pgtg_handle* h, bool final) {
   a.trunc = o.truncated;
   a.dst = final ? h->final_flat_dst : h->flat_dst;
   a.final = final ? 1 : 0;
-  // rows per workgroup <= 256; a grid of >= 2 048 workgroups where the batch allows
-  const uint64_t G = std::max<uint64_t>(std::min<uint64_t>(h->n, 2048), (h->n + 255) / 256);
-  if (h->flat_dtype) hipLaunchKernelGGL(k_flatten<int8_t>, dim3((unsigned)G), dim3(256), 0, h->stream, a);
-  else hipLaunchKernelGGL(k_flatten<float>, dim3((unsigned)G), dim3(256), 0, h->stream, a);
+  // rows per workgroup <= 256; one round of resident workgroups where the batch allows (6 per CU)
+  const uint64_t G = std::max<uint64_t>(std::min<uint64_t>(h->n, 1536), (h->n + 255) / 256);
+  // (float pairs per store, k_flatten<float, 2>: 94.7 vs 81.1 us per pass at 65 536 envs, not used)
+  if (h->flat_dtype) hipLaunchKernelGGL((k_flatten<int8_t, 1>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
+  else hipLaunchKernelGGL((k_flatten<float, 1>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
   HIPCHK(h, hipGetLastError());
   return PGTG_OK;
 }
