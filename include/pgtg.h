@@ -232,6 +232,11 @@ int pgtg_set_rules(pgtg_handle* h, const PgtgRule* rules, int32_t n_rules);
  * FlattenObservation wrapper the reference's caller puts around each env. */
 int pgtg_set_flat_outputs(pgtg_handle* h, const int32_t* order, int32_t n_order, int32_t dtype, void* flat_dev,
                           void* final_flat_dev);
+/* With flat rows bound, the observation pass of k_flatten also writes, per env, the reward as float32,
+ * done = terminated | truncated and truncated-and-not-terminated (uint8 0/1) -- what an SB3-style
+ * vector env returns -- into these [N] device buffers (all three or none; needs the reward, terminated
+ * and truncated outputs bound).  No reference function: it replaces per-step tensor arithmetic. */
+int pgtg_set_flat_scalars(pgtg_handle* h, float* reward_f32_dev, uint8_t* dones_dev, uint8_t* truncated_only_dev);
 /* Re-emit the observation of every env into the bound outputs (after set_agent/add_car). */
 int pgtg_observe(pgtg_handle* h);
 /* Per-env uint64 digest of the car list into out_dev[N] (device; parity tests: the car term of

@@ -32,7 +32,7 @@ EXPORTED = [
     "pgtg_get_map_plan", "pgtg_get_squares", "pgtg_set_rules", "pgtg_set_agent", "pgtg_add_car", "pgtg_observe", "pgtg_get_counters",
     "pgtg_error_count", "pgtg_window", "pgtg_num_envs", "pgtg_launch_info", "pgtg_occupancy", "pgtg_step_kernel", "pgtg_last_error", "pgtg_enable_timing",
     "pgtg_timing_read", "pgtg_measure_hbm", "pgtg_state_size", "pgtg_dump_state", "pgtg_load_state",
-    "pgtg_set_to_state", "pgtg_car_digest", "pgtg_get_queue_maps", "pgtg_get_queue_overflow", "pgtg_set_flat_outputs",
+    "pgtg_set_to_state", "pgtg_car_digest", "pgtg_get_queue_maps", "pgtg_get_queue_overflow", "pgtg_set_flat_outputs", "pgtg_set_flat_scalars",
 ]
 
 
@@ -132,6 +132,7 @@ def lib():
         "pgtg_get_queue_maps": ([vp, C.POINTER(u64)], C.c_int),
         "pgtg_get_queue_overflow": ([vp, C.POINTER(u64)], C.c_int),
         "pgtg_set_flat_outputs": ([vp, C.POINTER(C.c_int32), i32, i32, vp, vp], C.c_int),
+        "pgtg_set_flat_scalars": ([vp, vp, vp, vp], C.c_int),
         "pgtg_error_count": ([vp, C.POINTER(u64), C.POINTER(i32)], C.c_int),
         "pgtg_window": ([vp], C.c_int),
         "pgtg_num_envs": ([vp], u64),

@@ -4280,11 +4280,23 @@ struct FlatArgs {
   const uint8_t* term;
   const uint8_t* trunc;
   void* dst;
+  // the SB3 path's per-env scalars, written by the observation pass when bound (pgtg_set_flat_scalars):
+  // the reward as float32, done = terminated | truncated, and truncated-but-not-terminated
+  const double* rew;
+  float* rew32;
+  uint8_t* dones;
+  uint8_t* tonly;
+  // the terminal observation's set (final == 2: both passes in one launch)
+  const uint8_t* fobs;
+  const int32_t* fpos;
+  const int32_t* fvel;
+  const int32_t* fnsd;
+  void* fdst;
   uint64_t n;
-  int32_t D, OB, w2, cw2, nsd_on, final;
+  int32_t D, OB, w2, cw2, nsd_on, final;  // final: 0 the observation rows, 1 the terminal rows, 2 both
   uint8_t order[PGTG_MAX_CHANNELS];  // channel (in the observation) of the k-th name-sorted key
 };
-// One workgroup takes the rows b, b + G, b + 2G, ... of the grid's G workgroups (at most 256): it lists
+// One workgroup takes K consecutive rows (K = ceil(N / G) <= 256 for the grid's G workgroups): it lists
 // the rows to write (every row, or the finished envs' for the terminal rows) and its waves write them,
 // a row per wave.  A thread per 16 output bytes of the whole array,
 // the first version, spent its time in a 64-bit division and in launching 18 M threads, most of which
@@ -4317,7 +4329,7 @@ template <typename T, int V>
 __global__ void __launch_bounds__(256) k_flatten(FlatArgs a) {
   // obs byte offset of the row's first kFlatU x 64 values (channels in name order), built once
   __shared__ uint32_t offs[kFlatU * 64];
-  __shared__ uint32_t rows[256];
+  __shared__ uint32_t rows[512];  // t (observation row) or 256 + t (terminal row)
   __shared__ uint32_t nrows;
   const int t = threadIdx.x;
   const uint32_t D = (uint32_t)a.D, w2 = (uint32_t)a.w2, cw2 = (uint32_t)a.cw2;
@@ -4327,15 +4339,27 @@ __global__ void __launch_bounds__(256) k_flatten(FlatArgs a) {
   }
   if (t == 0) nrows = 0u;
   __syncthreads();
-  const uint64_t e = blockIdx.x + (uint64_t)t * gridDim.x;
-  bool keep = e < a.n;
-  if (keep && a.final) keep = (a.term[e] | a.trunc[e]) != 0;
-  const uint64_t m = __ballot(keep);
-  if (m) {
-    uint32_t base = 0;
-    if ((t & 63) == 0) base = atomicAdd(&nrows, (uint32_t)__popcll(m));
-    base = __shfl(base, 0);
-    if (keep) rows[base + __popcll(m & ((1ull << (t & 63)) - 1ull))] = (uint32_t)t;
+  // this workgroup's rows: K consecutive envs (coalesced flag reads and scalar writes, contiguous rows)
+  const uint64_t K = (a.n + gridDim.x - 1) / gridDim.x;  // <= 256 (launch_flatten)
+  const uint64_t e = (uint64_t)blockIdx.x * K + (uint64_t)t;
+  const bool valid = (uint64_t)t < K && e < a.n;
+  const bool done = valid && a.final != 0 && (a.term[e] | a.trunc[e]) != 0;
+  if (valid && a.final != 1 && a.dones) {
+    const uint8_t te = a.term[e], tr = a.trunc[e];
+    a.dones[e] = (uint8_t)((te | tr) != 0);
+    a.tonly[e] = (uint8_t)(tr != 0 && te == 0);
+    a.rew32[e] = (float)a.rew[e];
+  }
+#pragma unroll
+  for (int f = 0; f < 2; f++) {  // the observation rows, then the terminal rows
+    const bool keep = f == 0 ? (valid && a.final != 1) : done;
+    const uint64_t m = __ballot(keep);
+    if (m) {
+      uint32_t base = 0;
+      if ((t & 63) == 0) base = atomicAdd(&nrows, (uint32_t)__popcll(m));
+      base = __shfl(base, 0);
+      if (keep) rows[base + __popcll(m & ((1ull << (t & 63)) - 1ull))] = (uint32_t)t + 256u * (uint32_t)f;
+    }
   }
   __syncthreads();
   const uint32_t nr = nrows;
@@ -4346,11 +4370,15 @@ __global__ void __launch_bounds__(256) k_flatten(FlatArgs a) {
   using VT = typename FlatVec<T, V>::type;
   const int wv = t >> 6, ln = t & 63;
   for (uint32_t r = (uint32_t)wv; r < nr; r += 4u) {
-    const uint64_t er = blockIdx.x + (uint64_t)rows[r] * gridDim.x;
-    const uint8_t* __restrict__ orow = a.obs + er * (uint64_t)a.OB;
-    T* __restrict__ row = reinterpret_cast<T*>(a.dst) + er * (uint64_t)D;
-    const int nsdv = a.nsd_on ? a.nsd[er] + 1 : -1;
-    const int px = a.pos[2 * er], py = a.pos[2 * er + 1], vx = a.vel[2 * er], vy = a.vel[2 * er + 1];
+    const uint32_t ent = rows[r];
+    const bool fr = ent >= 256u;  // (uniform: one row per wave)
+    const uint64_t er = (uint64_t)blockIdx.x * K + (ent & 255u);
+    const uint8_t* __restrict__ orow = (fr ? a.fobs : a.obs) + er * (uint64_t)a.OB;
+    T* __restrict__ row = reinterpret_cast<T*>(fr ? a.fdst : a.dst) + er * (uint64_t)D;
+    const int32_t* pos = fr ? a.fpos : a.pos;
+    const int32_t* vel = fr ? a.fvel : a.vel;
+    const int nsdv = a.nsd_on ? (fr ? a.fnsd : a.nsd)[er] + 1 : -1;
+    const int px = pos[2 * er], py = pos[2 * er + 1], vx = vel[2 * er], vy = vel[2 * er + 1];
     for (uint32_t j0 = 0; j0 < D; j0 += kFlatU * 64u) {
       uint32_t ob[kFlatU];
 #pragma unroll
@@ -4423,6 +4451,9 @@ struct pgtg_handle {
   FlatArgs flat{};
   void* flat_dst = nullptr;
   void* final_flat_dst = nullptr;
+  float* flat_rew32 = nullptr;  // pgtg_set_flat_scalars
+  uint8_t* flat_dones = nullptr;
+  uint8_t* flat_tonly = nullptr;
   int flat_dtype = 0;  // 0 float32, 1 int8
 };
 
@@ -5146,9 +5177,11 @@ int pgtg_set_outputs(pgtg_handle* h, const PgtgOutputs* o) {
 }
 
 // k_flatten over the bound observation (final: the terminal observations, finished envs' rows only)
-static int launch_flatten(pgtg_handle* h, bool final) {
+// mode: 0 the observation rows, 1 the terminal rows, 2 both (one launch after a step)
+static int launch_flatten(pgtg_handle* h, int mode) {
   FlatArgs a = h->flat;
   const PgtgOutputs& o = h->out;
+  const bool final = mode == 1;
   a.obs = final ? o.final_obs : o.obs;
   a.pos = final ? o.final_position : o.position;
   a.vel = final ? o.final_velocity : o.velocity;
@@ -5156,7 +5189,16 @@ static int launch_flatten(pgtg_handle* h, bool final) {
   a.term = o.terminated;
   a.trunc = o.truncated;
   a.dst = final ? h->final_flat_dst : h->flat_dst;
-  a.final = final ? 1 : 0;
+  a.fobs = o.final_obs;
+  a.fpos = o.final_position;
+  a.fvel = o.final_velocity;
+  a.fnsd = o.final_next_subgoal;
+  a.fdst = h->final_flat_dst;
+  a.final = mode;
+  a.rew = o.reward;
+  a.rew32 = final ? nullptr : h->flat_rew32;
+  a.dones = final ? nullptr : h->flat_dones;
+  a.tonly = final ? nullptr : h->flat_tonly;
   // rows per workgroup <= 256; one round of resident workgroups where the batch allows (6 per CU)
   const uint64_t G = std::max<uint64_t>(std::min<uint64_t>(h->n, 1536), (h->n + 255) / 256);
   // (float pairs per store, k_flatten<float, 2>: 94.7 vs 81.1 us per pass at 65 536 envs, not used)
@@ -5203,11 +5245,10 @@ static int launch(pgtg_handle* h, const uint8_t* actions, const uint8_t* mask, i
     HIPCHK(h, hipGetLastError());
     h->tr_slot ^= 1u;
   }
-  if (h->flat_dst) {
-    if (int rc = launch_flatten(h, false)) return rc;
-  }
-  if (h->final_flat_dst && mode == MODE_STEP) {
-    if (int rc = launch_flatten(h, true)) return rc;
+  {
+    const bool fl = h->flat_dst != nullptr, ff = h->final_flat_dst != nullptr && mode == MODE_STEP;
+    if (fl || ff)  // (both row sets in one launch after a step)
+      if (int rc = launch_flatten(h, fl && ff ? 2 : (ff ? 1 : 0))) return rc;
   }
   if (timed) {
     HIPCHK(h, hipEventRecord(h->evpool[h->ev_used + 1], h->stream));
@@ -5766,6 +5807,21 @@ int pgtg_set_flat_outputs(pgtg_handle* h, const int32_t* order, int32_t n_order,
   h->flat_dtype = dtype;
   h->flat_dst = flat_dev;
   h->final_flat_dst = final_flat_dev;
+  return PGTG_OK;
+}
+
+int pgtg_set_flat_scalars(pgtg_handle* h, float* reward_f32_dev, uint8_t* dones_dev, uint8_t* truncated_only_dev) {
+  if (!h) return PGTG_E_INVALID;
+  h->flat_rew32 = nullptr;
+  h->flat_dones = h->flat_tonly = nullptr;
+  if (!reward_f32_dev && !dones_dev && !truncated_only_dev) return PGTG_OK;
+  if (!reward_f32_dev || !dones_dev || !truncated_only_dev)
+    return fail(h, PGTG_E_INVALID, "flat scalars: all three buffers or none");
+  if (!h->out.reward || !h->out.terminated || !h->out.truncated)
+    return fail(h, PGTG_E_INVALID, "flat scalars need the reward, terminated and truncated outputs");
+  h->flat_rew32 = reward_f32_dev;
+  h->flat_dones = dones_dev;
+  h->flat_tonly = truncated_only_dev;
   return PGTG_OK;
 }
 

@@ -178,6 +178,8 @@ class PGTGSB3VecEnv:
 
     def reset(self):
         if self._kernel_flat():
+            if self.device_obs:  # (the reset's observation pass must not write into the last step's scalars)
+                self.venv.set_flat_scalars(None, None, None)
             flat, _ = self._bind_flat(final=False)
             self.venv.reset(seed=self._seed)
         else:
@@ -211,6 +213,11 @@ class PGTGSB3VecEnv:
         kflat = self._kernel_flat()
         if kflat:  # the rows are written by k_flatten in the step: no torch work on the observations
             flat_d, final_d = self._bind_flat(final=True)
+            if self.device_obs:  # ... nor on the rewards and done flags (written by the same pass)
+                n, dev = self.num_envs, self.venv.device
+                sc = (torch.empty(n, dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.bool, device=dev),
+                      torch.empty(n, dtype=torch.bool, device=dev))
+                self.venv._bind_flat_scalar_ptrs(*sc)
             self.venv.step_launch(self._actions)
             v = self.venv
             reward, term, trunc, infos = v.reward, v.terminated, v.truncated, {}
@@ -218,6 +225,12 @@ class PGTGSB3VecEnv:
                 infos["cost"] = v.cost
         else:
             obs, reward, term, trunc, infos = self.venv.step(self._actions)
+        if self.device_obs and kflat:
+            cost = infos.get("cost")
+            if cost is not None:  # (the venv's output buffer, rewritten by the next step)
+                cost = cost.clone()
+            rew32, dones, tonly = sc
+            return flat_d, rew32, dones, DeviceVecInfos(dones, tonly, final_d, cost)
         if self.device_obs:
             dones = term | trunc
             if kflat:

@@ -257,6 +257,28 @@ class PGTGVecEnv:
         self._flat_order = (C.c_int32 * len(order))(*order)
         self._bind_flat_ptrs(flat, final_flat, 0 if dt == torch.float32 else 1)
 
+    def set_flat_scalars(self, reward_f32=None, dones=None, truncated_only=None) -> None:
+        """With flat rows bound, every observation pass also writes the reward as float32, done =
+        terminated | truncated and truncated-and-not-terminated into these [N] device tensors (float32,
+        bool, bool; include/pgtg.h pgtg_set_flat_scalars).  None, None, None unbinds."""
+        import torch
+        ts = (reward_f32, dones, truncated_only)
+        if all(t is None for t in ts):
+            _check(self._lib.pgtg_set_flat_scalars(self._h, None, None, None), self._h)
+            self._flat_scalar_refs = ()
+            return
+        if any(t is None for t in ts):
+            raise ValueError("flat scalars: all three tensors or none")
+        for t, dt in zip(ts, (torch.float32, torch.bool, torch.bool)):
+            if t.dtype != dt or tuple(t.shape) != (self.num_envs,) or not t.is_contiguous() or t.device != self.device:
+                raise ValueError(f"flat scalars: contiguous [{self.num_envs}] {dt} tensors on {self.device}")
+        self._bind_flat_scalar_ptrs(*ts)
+
+    def _bind_flat_scalar_ptrs(self, reward_f32, dones, truncated_only) -> None:
+        _check(self._lib.pgtg_set_flat_scalars(self._h, C.c_void_p(reward_f32.data_ptr()), C.c_void_p(dones.data_ptr()),
+                                               C.c_void_p(truncated_only.data_ptr())), self._h)
+        self._flat_scalar_refs = (reward_f32, dones, truncated_only)
+
     def _bind_flat_ptrs(self, flat, final_flat, dtype_code: int) -> None:
         """Rebind flat rows already checked by set_flat_outputs (same shape and dtype): the per-step
         path of PGTGSB3VecEnv, which hands out fresh tensors every step."""

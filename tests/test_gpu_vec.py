@@ -204,6 +204,10 @@ def test_flat_rows_kernel_equals_flatten_obs(dtype):
     env.set_flat_outputs(flat, fin)
     env.reset(seed=11)
     assert torch.equal(flat, flatten_obs(spec, env.observation(), dtype=dtype))
+    # the per-env scalars of the same pass (pgtg_set_flat_scalars)
+    r32, dn, to = (torch.empty(N, dtype=torch.float32, device="cuda"), torch.empty(N, dtype=torch.bool, device="cuda"),
+                   torch.empty(N, dtype=torch.bool, device="cuda"))
+    env.set_flat_scalars(r32, dn, to)
     g = torch.Generator(device="cuda").manual_seed(4)
     finished = 0
     for t in range(T):
@@ -211,6 +215,8 @@ def test_flat_rows_kernel_equals_flatten_obs(dtype):
         env.step(torch.randint(0, 9, (N,), device="cuda", dtype=torch.uint8, generator=g))
         assert torch.equal(flat, flatten_obs(spec, env.observation(), dtype=dtype)), t
         done = env.terminated | env.truncated
+        assert torch.equal(r32, env.reward.to(torch.float32)) and torch.equal(dn, done), t
+        assert torch.equal(to, env.truncated & ~env.terminated), t
         want = flatten_obs(spec, env.final_observation(), dtype=dtype)
         assert torch.equal(fin[done], want[done]), t
         assert bool((fin[~done] == 77).all()), t
