@@ -4311,22 +4311,25 @@ __device__ __forceinline__ T flat_tail(const FlatArgs& a, int k, int nsdv, int p
   if (k < 18) return (T)(k - 9 == py ? 1 : 0);
   return (T)(k == 18 ? vx : vy);
 }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kFlatU = 18;  // values per lane in one pass of a row: rows of up to 18 x 64 = 1 152 in one pass
-// V consecutive values per lane and store (V = 2: float pairs, rows of an even D are 8-byte aligned)
-template <typename T, int V>
-struct FlatVec;
-template <>
-struct FlatVec<float, 2> {
-  using type = float2;
-  __device__ static float2 make(const float* f) { return make_float2(f[0], f[1]); }
-};
-template <typename T>
-struct FlatVec<T, 1> {
-  using type = T;
-  __device__ static T make(const T* f) { return f[0]; }
-};
-template <typename T, int V>
-__global__ void __launch_bounds__(256) k_flatten(FlatArgs a) {
+// a wave-uniform pointer the compiler can see is uniform (its halves through readfirstlane), so that a
+// buffer descriptor built from it sits in scalar registers without a per-access waterfall loop
+__device__ __forceinline__ void* uniform_ptr(const void* p) {
+  const uint64_t u = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return (void*)(uintptr_t)((uint64_t)hi << 32 | lo);
+}
+__device__ __forceinline__ void flat_store(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void flat_store(__amdgpu_buffer_rsrc_t r, uint32_t off, int8_t v) {
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, off, 0, 0);
+}
+// ONE: rows of at most kFlatU x 64 values (one pass per row, software-pipelined); otherwise rows in
+// passes of kFlatU x 64 values
+template <typename T, bool ONE>
+__global__ void __launch_bounds__(256, 6) k_flatten(FlatArgs a) {
   // obs byte offset of the row's first kFlatU x 64 values (channels in name order), built once
   __shared__ uint32_t offs[kFlatU * 64];
   __shared__ uint32_t rows[512];  // t (observation row) or 256 + t (terminal row)
@@ -4362,40 +4365,142 @@ __global__ void __launch_bounds__(256) k_flatten(FlatArgs a) {
     }
   }
   __syncthreads();
-  const uint32_t nr = nrows;
-  // one row per wave at a time (the workgroup's four waves on four rows): every load of a pass -- the
-  // observation bytes and the tail's scalars -- issued before its first store, so a row of <= 1 152
-  // values costs one memory round trip; lane l writes values V(l + 64k) .. V(l + 64k) + V - 1
-  constexpr int P = kFlatU / V;  // stores per lane and pass
-  using VT = typename FlatVec<T, V>::type;
-  const int wv = t >> 6, ln = t & 63;
-  for (uint32_t r = (uint32_t)wv; r < nr; r += 4u) {
-    const uint32_t ent = rows[r];
-    const bool fr = ent >= 256u;  // (uniform: one row per wave)
-    const uint64_t er = (uint64_t)blockIdx.x * K + (ent & 255u);
-    const uint8_t* __restrict__ orow = (fr ? a.fobs : a.obs) + er * (uint64_t)a.OB;
-    T* __restrict__ row = reinterpret_cast<T*>(fr ? a.fdst : a.dst) + er * (uint64_t)D;
-    const int32_t* pos = fr ? a.fpos : a.pos;
-    const int32_t* vel = fr ? a.fvel : a.vel;
-    const int nsdv = a.nsd_on ? (fr ? a.fnsd : a.nsd)[er] + 1 : -1;
-    const int px = pos[2 * er], py = pos[2 * er + 1], vx = vel[2 * er], vy = vel[2 * er + 1];
-    for (uint32_t j0 = 0; j0 < D; j0 += kFlatU * 64u) {
-      uint32_t ob[kFlatU];
+  // one row per wave at a time (the workgroup's four waves on four rows), and every load of a row --
+  // the observation bytes and the tail's scalars -- issued before its first store
+  const int ln = t & 63;
+  // (the row loop's bounds made visibly uniform: its branches and the descriptors stay scalar)
+  const uint32_t nr = __builtin_amdgcn_readfirstlane(nrows);
+  const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)(t >> 6));
+  if constexpr (ONE) {
+    // Software-pipelined: the next row's loads are issued before this row's stores.  (gfx9 counts
+    // loads and stores on one in-order counter, so a wave that loads after storing waits for its
+    // stores to drain; here the wait for row r + 4's bytes lets row r's stores stay in flight.)
+    // A row's observation bytes arrive with two 16-byte loads per lane into registers, go through the
+    // wave's LDS window, and come back in name order with byte reads: per row 2 + 1 loads instead of
+    // one byte load per value, the memory pipeline's instructions being what bounds this kernel.
+    // Buffer loads and stores through per-row descriptors built from wave-uniform values; the range
+    // check drops the lanes past a row's end (per dword, so the row's last bytes when OB % 4 != 0 come
+    // with a byte load of their own).
+    __shared__ u32x4 win[4][128];  // per wave: a row's observation bytes (<= 2 048)
+    uint8_t* wb = reinterpret_cast<uint8_t*>(&win[wv][0]);
+    struct Row {
+      u32x4 q0, q1;  // observation bytes 16 ln .. and 1 024 + 16 ln ..
+      uint32_t tb;   // byte OB & ~3 + ln (lanes below OB % 4)
+      int mv[3];     // summed: lanes 0..4 the row's x, y, vx, vy, next subgoal (read back with readlane)
+      __amdgpu_buffer_rsrc_t dst;
+      __amdgpu_buffer_rsrc_t dsto;  // the row's chunks below pb
+    };
+    const uint32_t lo = (uint32_t)ln * (uint32_t)sizeof(T);
+    const uint32_t pb = cw2 / 64u;  // the chunk of 64 values where the tail starts
+    const uint32_t OB = (uint32_t)a.OB, obt = OB & ~3u;
+    // the scalars' lane offsets: lane 0-1 in the 8 position bytes, 2-3 in the velocity's, 4 in the next
+    // subgoal's; every other lane past its descriptor's end (without 32-bit wrap-around)
+    const uint32_t lo4 = (uint32_t)ln * 4u, ovel = ln >= 2 ? lo4 - 8u : 1u << 20, onsd = ln >= 4 ? lo4 - 16u : 1u << 20;
+    uint32_t offv[kFlatU + 1];  // this lane's source offsets: chunks 0 .. kFlatU - 1, then chunk pb
 #pragma unroll
-      for (int u = 0; u < kFlatU; u++) {
-        const uint32_t j = j0 + (uint32_t)V * ((uint32_t)ln + (uint32_t)(u / V) * 64u) + (uint32_t)(u % V);
-        const uint32_t jj = j - j0;  // (< kFlatU x 64)
-        const uint32_t off = j0 == 0 ? offs[jj] : (j < cw2 ? (uint32_t)a.order[j / w2] * w2 + j % w2 : 0u);
-        ob[u] = orow[j < cw2 ? off : 0u];  // (unconditional: one batch of loads)
+    for (int u = 0; u <= kFlatU; u++) {
+      const uint32_t j = (uint32_t)ln + (u == kFlatU ? pb : (uint32_t)u) * 64u;
+      offv[u] = j < cw2 ? offs[j] : 0u;
+    }
+    auto load_row = [&](uint32_t r, Row& m) {
+      const uint32_t ent = __builtin_amdgcn_readfirstlane(rows[r]);
+      const bool fr = ent >= 256u;
+      const uint64_t er = (uint64_t)blockIdx.x * K + (ent & 255u);
+      const uint8_t* orow = (fr ? a.fobs : a.obs) + er * (uint64_t)OB;
+      T* row = reinterpret_cast<T*>(fr ? a.fdst : a.dst) + er * (uint64_t)D;
+      const auto src = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(orow), 0, (int)OB, 0x00020000);
+      m.dst = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(row), 0,
+                                                __builtin_amdgcn_readfirstlane((int)(D * sizeof(T))), 0x00020000);
+      m.dsto = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(row), 0,
+                                                 __builtin_amdgcn_readfirstlane((int)(pb * 64u * sizeof(T))), 0x00020000);
+      // (three dword loads through descriptors of 8, 8 and 4 bytes: the range check gives the other
+      // lanes 0, so the sum has x, y in lanes 0-1, vx, vy in 2-3 and the next subgoal in lane 4)
+      const auto dpos = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr((fr ? a.fpos : a.pos) + 2 * er), 0, 8, 0x00020000);
+      const auto dvel = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr((fr ? a.fvel : a.vel) + 2 * er), 0, 8, 0x00020000);
+      const auto dnsd = __builtin_amdgcn_make_buffer_rsrc(
+          uniform_ptr(a.nsd_on ? (fr ? a.fnsd : a.nsd) + er : (fr ? a.fpos : a.pos)), 0, a.nsd_on ? 4 : 0, 0x00020000);
+      // (summed where the row is stored: an add here would wait for the loads just issued)
+      m.mv[0] = (int)__builtin_amdgcn_raw_buffer_load_b32(dpos, lo4, 0, 0);
+      m.mv[1] = (int)__builtin_amdgcn_raw_buffer_load_b32(dvel, ovel, 0, 0);
+      m.mv[2] = (int)__builtin_amdgcn_raw_buffer_load_b32(dnsd, onsd, 0, 0);
+      m.q0 = __builtin_amdgcn_raw_buffer_load_b128(src, lo4 * 4u, 0, 0);
+      m.q1 = __builtin_amdgcn_raw_buffer_load_b128(src, 1024u + lo4 * 4u, 0, 0);
+      m.tb = __builtin_amdgcn_raw_buffer_load_b8(src, obt + (uint32_t)ln, 0, 0);
+    };
+    auto store_row = [&](const Row& m) {
+      win[wv][ln] = m.q0;
+      win[wv][64 + ln] = m.q1;
+      if ((uint32_t)ln < OB - obt) wb[obt + (uint32_t)ln] = (uint8_t)m.tb;  // (after the 16-byte writes)
+      const int mv = m.mv[0] + m.mv[1] + m.mv[2];
+      const int px = __builtin_amdgcn_readlane(mv, 0), py = __builtin_amdgcn_readlane(mv, 1);
+      const int vx = __builtin_amdgcn_readlane(mv, 2), vy = __builtin_amdgcn_readlane(mv, 3);
+      const int nsdv = __builtin_amdgcn_readlane(mv, 4) + 1;
+      // the chunks of 64 values below the tail's chunk pb hold observation bytes only; chunk pb holds
+      // the last ones (lanes below cw2) and the tail's start, chunk pb + 1 the tail's rest (<= 29 values)
+      // (the first through a descriptor ending at chunk pb: the range check drops the rest, no branches)
+#pragma unroll
+      for (int p = 0; p < kFlatU; p++) flat_store(m.dsto, lo + (uint32_t)(p * 64 * (int)sizeof(T)), (T)wb[offv[p]]);
+      const uint32_t obb = wb[offv[kFlatU]];  // chunk pb's observation byte
+#pragma unroll
+      for (int s = 0; s < 2; s++) {
+        const uint32_t pc = pb + (uint32_t)s;
+        const int k = ln + (int)pc * 64 - (int)cw2;  // tail index of this lane's value (< 0: observation)
+        const int k2 = a.nsd_on ? k - 9 : k;
+        int tv = (int)(k2 == px);
+        tv = k2 < 9 ? tv : (int)(k2 - 9 == py);
+        tv = k2 < 18 ? tv : (k2 == 18 ? vx : vy);
+        tv = (a.nsd_on && k < 9) ? (int)(k == nsdv) : tv;
+        const T f = k < 0 ? (T)obb : (T)tv;
+        if (pc * 64u < D) flat_store(m.dst, lo + pc * 64u * (uint32_t)sizeof(T), f);  // (lanes past D dropped)
       }
+    };
+    // Two rows per iteration: the registers alternate without copies.  The next row's loads are
+    // unconditional (the last row re-read at the end), and the first row is peeled off, so that every
+    // path into a row's stores has the same loads and stores outstanding: the compiler's counter
+    // waits then leave the previous row's stores in flight (a path without them, the first row's,
+    // merged into the loop made it wait for every earlier store).
+    Row mA{}, mB{};
+    uint32_t r = wv;
+    if (r < nr) {
+      load_row(r, mA);
+      load_row(min(r + 4u, nr - 1u), mB);
+      store_row(mA);
+      r += 4u;
+      while (r < nr) {  // (mB holds row r)
+        load_row(min(r + 4u, nr - 1u), mA);
+        store_row(mB);
+        r += 4u;
+        if (r >= nr) break;
+        load_row(min(r + 4u, nr - 1u), mB);
+        store_row(mA);
+        r += 4u;
+      }
+    }
+  } else {
+    for (uint32_t r = wv; r < nr; r += 4u) {
+      const uint32_t ent = rows[r];
+      const bool fr = ent >= 256u;  // (uniform: one row per wave)
+      const uint64_t er = (uint64_t)blockIdx.x * K + (ent & 255u);
+      const uint8_t* __restrict__ orow = (fr ? a.fobs : a.obs) + er * (uint64_t)a.OB;
+      T* __restrict__ row = reinterpret_cast<T*>(fr ? a.fdst : a.dst) + er * (uint64_t)D;
+      const int32_t* pos = fr ? a.fpos : a.pos;
+      const int32_t* vel = fr ? a.fvel : a.vel;
+      const int nsdv = a.nsd_on ? (fr ? a.fnsd : a.nsd)[er] + 1 : -1;
+      const int px = pos[2 * er], py = pos[2 * er + 1], vx = vel[2 * er], vy = vel[2 * er + 1];
+      for (uint32_t j0 = 0; j0 < D; j0 += kFlatU * 64u) {  // a pass: kFlatU loads per lane, then the stores
+        uint32_t ob[kFlatU];
 #pragma unroll
-      for (int p = 0; p < P; p++) {
-        const uint32_t j = j0 + (uint32_t)V * ((uint32_t)ln + (uint32_t)p * 64u);
-        T f[V];
+        for (int u = 0; u < kFlatU; u++) {
+          const uint32_t j = j0 + (uint32_t)ln + (uint32_t)u * 64u;
+          const uint32_t off = j0 == 0 ? offs[j - j0] : (j < cw2 ? (uint32_t)a.order[j / w2] * w2 + j % w2 : 0u);
+          ob[u] = orow[j < cw2 ? off : 0u];  // (unconditional: one batch of loads)
+        }
 #pragma unroll
-        for (int h = 0; h < V; h++)
-          f[h] = j + h < cw2 ? (T)ob[p * V + h] : flat_tail<T>(a, (int)(j + h - cw2), nsdv, px, py, vx, vy);
-        if (j < D) *reinterpret_cast<VT*>(row + j) = FlatVec<T, V>::make(f);  // (D % V == 0)
+        for (int p = 0; p < kFlatU; p++) {
+          const uint32_t j = j0 + (uint32_t)ln + (uint32_t)p * 64u;
+          const T f = j < cw2 ? (T)ob[p] : flat_tail<T>(a, (int)(j - cw2), nsdv, px, py, vx, vy);
+          if (j < D) row[j] = f;
+        }
       }
     }
   }
@@ -4449,6 +4554,8 @@ struct pgtg_handle {
   int tune_queue_mode = 0;  // PgtgConfig.tune_queue_mode
   // FlattenObservation rows after every launch (pgtg_set_flat_outputs): k_flatten's arguments
   FlatArgs flat{};
+  const void* flat_fn = nullptr;  // k_flatten variant of the last launch, and its resident workgroups
+  uint64_t flat_wgs = 1536;
   void* flat_dst = nullptr;
   void* final_flat_dst = nullptr;
   float* flat_rew32 = nullptr;  // pgtg_set_flat_scalars
@@ -5199,11 +5306,28 @@ static int launch_flatten(pgtg_handle* h, int mode) {
   a.rew32 = final ? nullptr : h->flat_rew32;
   a.dones = final ? nullptr : h->flat_dones;
   a.tonly = final ? nullptr : h->flat_tonly;
-  // rows per workgroup <= 256; one round of resident workgroups where the batch allows (6 per CU)
-  const uint64_t G = std::max<uint64_t>(std::min<uint64_t>(h->n, 1536), (h->n + 255) / 256);
-  // (float pairs per store, k_flatten<float, 2>: 94.7 vs 81.1 us per pass at 65 536 envs, not used)
-  if (h->flat_dtype) hipLaunchKernelGGL((k_flatten<int8_t, 1>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
-  else hipLaunchKernelGGL((k_flatten<float, 1>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
+  // (float pairs per store: 94.7 vs 81.1 us per pass at 65 536 envs, not kept)
+  const bool one = a.D <= kFlatU * 64;
+  const void* fn = h->flat_dtype ? (one ? (const void*)k_flatten<int8_t, true> : (const void*)k_flatten<int8_t, false>)
+                                 : (one ? (const void*)k_flatten<float, true> : (const void*)k_flatten<float, false>);
+  if (h->flat_fn != fn) {  // the workgroups resident at once (kernel registers), fixed per variant
+    int ncu = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || ncu < 1) ncu = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    h->flat_fn = fn;
+    h->flat_wgs = (uint64_t)ncu * (uint64_t)per_cu;
+  }
+  // rows per workgroup <= 256; one round of resident workgroups where the batch allows.  (The grid
+  // hardly matters: 256 / 512 / 1 536 / 3 072 workgroups 150 / 138 / 139 / 134 us per step at 65 536
+  // envs, profiles/r06/flat_grid_sweep.txt -- the kernel is bound chip-wide, not by waves in flight)
+  const uint64_t G = std::max<uint64_t>(std::min<uint64_t>(h->n, h->flat_wgs), (h->n + 255) / 256);
+  if (h->flat_dtype) {
+    if (one) hipLaunchKernelGGL((k_flatten<int8_t, true>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
+    else hipLaunchKernelGGL((k_flatten<int8_t, false>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
+  } else {
+    if (one) hipLaunchKernelGGL((k_flatten<float, true>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
+    else hipLaunchKernelGGL((k_flatten<float, false>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
+  }
   HIPCHK(h, hipGetLastError());
   return PGTG_OK;
 }
