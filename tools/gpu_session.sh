@@ -26,6 +26,10 @@
 #   libtests:<lib>:<expr>  pytest -m gpu -k <expr> against another build of the library (PGTG_LIB)
 #   pmc:<wl>:<lib|new>     FETCH_SIZE / WRITE_SIZE passes of one workload with a given library
 #   sq:<wl>          SQ instruction/stall passes of one workload -> gpurun_out/<tag>/sq_<wl>.json (issue roofline)
+# Round-end records (profiles/r06/final) came from three calls:
+#   tests smoke bench driver benchlong:cfg2 benchlong:cfg3 benchlong:cfg4 benchlong:train shards rccl
+#   profile:cfg5,cfg2 stampsjson:cfg2 adapter ranks
+#   tests smoke bench driver adapter            (after the last k_flatten change)
 set -o pipefail
 TAG=$1
 shift
