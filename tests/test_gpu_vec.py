@@ -183,18 +183,32 @@ def test_step_kernel_occupancy(n, kw, want):
         vec.close()
 
 
+_FLAT_LAYOUTS = {
+    # the caller's settings (pgtg/train.py:21-40): D = 1 118, rows of one pass, next-subgoal one-hot
+    "caller": dict(random_map_width=4, random_map_height=4, random_map_obstacle_probability=0.2,
+                   random_map_percentage_of_connections=0.8, traffic_density=0.2, use_sliding_observation_window=True,
+                   sliding_observation_window_size=5, use_next_subgoal_direction=True),
+    # D = 461 (441 observation bytes), no next-subgoal one-hot: the tail starts inside chunk 6
+    "window3": dict(random_map_width=3, random_map_height=3, traffic_density=0.1, use_sliding_observation_window=True,
+                    sliding_observation_window_size=3),
+    # D = 2 054: rows in passes of 1 152 values (k_flatten<T, false>)
+    "window7": dict(random_map_width=3, random_map_height=3, use_sliding_observation_window=True,
+                    sliding_observation_window_size=7, use_next_subgoal_direction=True),
+}
+
+
+@pytest.mark.parametrize("layout", list(_FLAT_LAYOUTS))
 @pytest.mark.parametrize("dtype", [torch.float32, torch.int8])
-def test_flat_rows_kernel_equals_flatten_obs(dtype):
+def test_flat_rows_kernel_equals_flatten_obs(dtype, layout):
     """k_flatten (include/pgtg.h pgtg_set_flat_outputs: the FlattenObservation rows written inside the
     step) against flatten_obs, gymnasium's layout: every env's row of the observation after reset and
-    each of 30 steps, and the terminal rows of the finished envs (the others untouched), on the
-    caller's settings (pgtg/train.py:21-40) with the default feature list, whose name order differs
-    from the observation's channel order, over a multi-workgroup batch."""
+    each of 30 steps, and the terminal rows of the finished envs (the others untouched), with the
+    default feature list, whose name order differs from the observation's channel order, over a
+    multi-workgroup batch; three row layouts (one pass with and without the next-subgoal one-hot,
+    several passes)."""
     from pgtg_amd.flat import flat_dim
     from pgtg_amd.vector import PGTGVecEnv
-    spec = _spec(random_map_width=4, random_map_height=4, random_map_obstacle_probability=0.2,
-                 random_map_percentage_of_connections=0.8, traffic_density=0.2, use_sliding_observation_window=True,
-                 sliding_observation_window_size=5, use_next_subgoal_direction=True)
+    spec = _spec(**_FLAT_LAYOUTS[layout])
     assert [k for k, _ in spec.channels] != sorted(k for k, _ in spec.channels)
     N, T = 3000, 30
     env = PGTGVecEnv(N, spec=spec, device=0, autoreset=True, max_episode_steps=7)
