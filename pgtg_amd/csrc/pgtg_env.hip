@@ -5307,7 +5307,7 @@ static int launch_flatten(pgtg_handle* h, int mode) {
   a.dones = final ? nullptr : h->flat_dones;
   a.tonly = final ? nullptr : h->flat_tonly;
   // (float pairs per store: 94.7 vs 81.1 us per pass at 65 536 envs, not kept)
-  const bool one = a.D <= kFlatU * 64;
+  const bool one = a.D <= kFlatU * 64 && a.OB <= 2048;  // (rows of one pass; the bytes fit the LDS window)
   const void* fn = h->flat_dtype ? (one ? (const void*)k_flatten<int8_t, true> : (const void*)k_flatten<int8_t, false>)
                                  : (one ? (const void*)k_flatten<float, true> : (const void*)k_flatten<float, false>);
   if (h->flat_fn != fn) {  // the workgroups resident at once (kernel registers), fixed per variant
