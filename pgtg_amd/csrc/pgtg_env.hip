@@ -4326,9 +4326,20 @@ __device__ __forceinline__ void flat_store(__amdgpu_buffer_rsrc_t r, uint32_t of
 __device__ __forceinline__ void flat_store(__amdgpu_buffer_rsrc_t r, uint32_t off, int8_t v) {
   __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, off, 0, 0);
 }
+template <typename T, int V>
+__device__ __forceinline__ void flat_store_v(__amdgpu_buffer_rsrc_t r, uint32_t off, const T (&f)[V]) {
+  if constexpr (V == 1) {
+    flat_store(r, off, f[0]);
+  } else {
+    static_assert(V == 2 && sizeof(T) == 4, "pairs of float32 only");
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 x = {__builtin_bit_cast(uint32_t, f[0]), __builtin_bit_cast(uint32_t, f[1])};
+    __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, 0);
+  }
+}
 // ONE: rows of at most kFlatU x 64 values (one pass per row, software-pipelined); otherwise rows in
 // passes of kFlatU x 64 values
-template <typename T, bool ONE>
+template <typename T, bool ONE, int V>
 __global__ void __launch_bounds__(256, 6) k_flatten(FlatArgs a) {
   // obs byte offset of the row's first kFlatU x 64 values (channels in name order), built once
   __shared__ uint32_t offs[kFlatU * 64];
@@ -4390,18 +4401,23 @@ __global__ void __launch_bounds__(256, 6) k_flatten(FlatArgs a) {
       __amdgpu_buffer_rsrc_t dst;
       __amdgpu_buffer_rsrc_t dsto;  // the row's chunks below pb
     };
-    const uint32_t lo = (uint32_t)ln * (uint32_t)sizeof(T);
-    const uint32_t pb = cw2 / 64u;  // the chunk of 64 values where the tail starts
+    // V consecutive values per lane and store (V = 2: float pairs, rows of an even D), chunks of 64 V
+    constexpr int NC = kFlatU / V;
+    constexpr uint32_t CH = 64u * (uint32_t)V;
+    const uint32_t lo = (uint32_t)ln * (uint32_t)(V * sizeof(T));
+    const uint32_t pb = cw2 / CH;  // the chunk where the tail starts
     const uint32_t OB = (uint32_t)a.OB, obt = OB & ~3u;
     // the scalars' lane offsets: lane 0-1 in the 8 position bytes, 2-3 in the velocity's, 4 in the next
     // subgoal's; every other lane past its descriptor's end (without 32-bit wrap-around)
     const uint32_t lo4 = (uint32_t)ln * 4u, ovel = ln >= 2 ? lo4 - 8u : 1u << 20, onsd = ln >= 4 ? lo4 - 16u : 1u << 20;
-    uint32_t offv[kFlatU + 1];  // this lane's source offsets: chunks 0 .. kFlatU - 1, then chunk pb
+    uint32_t offv[NC + 1][V];  // this lane's source offsets: chunks 0 .. NC - 1, then chunk pb
 #pragma unroll
-    for (int u = 0; u <= kFlatU; u++) {
-      const uint32_t j = (uint32_t)ln + (u == kFlatU ? pb : (uint32_t)u) * 64u;
-      offv[u] = j < cw2 ? offs[j] : 0u;
-    }
+    for (int u = 0; u <= NC; u++)
+#pragma unroll
+      for (int h = 0; h < V; h++) {
+        const uint32_t j = (uint32_t)(V * ln + h) + (u == NC ? pb : (uint32_t)u) * CH;
+        offv[u][h] = j < cw2 ? offs[j] : 0u;
+      }
     auto load_row = [&](uint32_t r, Row& m) {
       const uint32_t ent = __builtin_amdgcn_readfirstlane(rows[r]);
       const bool fr = ent >= 256u;
@@ -4412,7 +4428,7 @@ __global__ void __launch_bounds__(256, 6) k_flatten(FlatArgs a) {
       m.dst = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(row), 0,
                                                 __builtin_amdgcn_readfirstlane((int)(D * sizeof(T))), 0x00020000);
       m.dsto = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(row), 0,
-                                                 __builtin_amdgcn_readfirstlane((int)(pb * 64u * sizeof(T))), 0x00020000);
+                                                 __builtin_amdgcn_readfirstlane((int)(pb * CH * sizeof(T))), 0x00020000);
       // (three dword loads through descriptors of 8, 8 and 4 bytes: the range check gives the other
       // lanes 0, so the sum has x, y in lanes 0-1, vx, vy in 2-3 and the next subgoal in lane 4)
       const auto dpos = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr((fr ? a.fpos : a.pos) + 2 * er), 0, 8, 0x00020000);
@@ -4435,23 +4451,34 @@ __global__ void __launch_bounds__(256, 6) k_flatten(FlatArgs a) {
       const int px = __builtin_amdgcn_readlane(mv, 0), py = __builtin_amdgcn_readlane(mv, 1);
       const int vx = __builtin_amdgcn_readlane(mv, 2), vy = __builtin_amdgcn_readlane(mv, 3);
       const int nsdv = __builtin_amdgcn_readlane(mv, 4) + 1;
-      // the chunks of 64 values below the tail's chunk pb hold observation bytes only; chunk pb holds
-      // the last ones (lanes below cw2) and the tail's start, chunk pb + 1 the tail's rest (<= 29 values)
+      // the chunks below the tail's chunk pb hold observation bytes only; chunk pb holds the last
+      // ones and the tail's start, chunk pb + 1 the tail's rest (<= 29 values)
       // (the first through a descriptor ending at chunk pb: the range check drops the rest, no branches)
 #pragma unroll
-      for (int p = 0; p < kFlatU; p++) flat_store(m.dsto, lo + (uint32_t)(p * 64 * (int)sizeof(T)), (T)wb[offv[p]]);
-      const uint32_t obb = wb[offv[kFlatU]];  // chunk pb's observation byte
+      for (int p = 0; p < NC; p++) {
+        T f[V];
+#pragma unroll
+        for (int h = 0; h < V; h++) f[h] = (T)wb[offv[p][h]];
+        flat_store_v<T, V>(m.dsto, lo + (uint32_t)p * CH * (uint32_t)sizeof(T), f);
+      }
+      uint32_t obb[V];  // chunk pb's observation bytes
+#pragma unroll
+      for (int h = 0; h < V; h++) obb[h] = wb[offv[NC][h]];
 #pragma unroll
       for (int s = 0; s < 2; s++) {
         const uint32_t pc = pb + (uint32_t)s;
-        const int k = ln + (int)pc * 64 - (int)cw2;  // tail index of this lane's value (< 0: observation)
-        const int k2 = a.nsd_on ? k - 9 : k;
-        int tv = (int)(k2 == px);
-        tv = k2 < 9 ? tv : (int)(k2 - 9 == py);
-        tv = k2 < 18 ? tv : (k2 == 18 ? vx : vy);
-        tv = (a.nsd_on && k < 9) ? (int)(k == nsdv) : tv;
-        const T f = k < 0 ? (T)obb : (T)tv;
-        if (pc * 64u < D) flat_store(m.dst, lo + pc * 64u * (uint32_t)sizeof(T), f);  // (lanes past D dropped)
+        T f[V];
+#pragma unroll
+        for (int h = 0; h < V; h++) {
+          const int k = V * ln + h + (int)(pc * CH) - (int)cw2;  // tail index of the value (< 0: observation)
+          const int k2 = a.nsd_on ? k - 9 : k;
+          int tv = (int)(k2 == px);
+          tv = k2 < 9 ? tv : (int)(k2 - 9 == py);
+          tv = k2 < 18 ? tv : (k2 == 18 ? vx : vy);
+          tv = (a.nsd_on && k < 9) ? (int)(k == nsdv) : tv;
+          f[h] = k < 0 ? (T)obb[h] : (T)tv;
+        }
+        if (pc * CH < D) flat_store_v<T, V>(m.dst, lo + pc * CH * (uint32_t)sizeof(T), f);  // (lanes past D dropped)
       }
     };
     // Two rows per iteration: the registers alternate without copies.  The next row's loads are
@@ -5306,10 +5333,13 @@ static int launch_flatten(pgtg_handle* h, int mode) {
   a.rew32 = final ? nullptr : h->flat_rew32;
   a.dones = final ? nullptr : h->flat_dones;
   a.tonly = final ? nullptr : h->flat_tonly;
-  // (float pairs per store: 94.7 vs 81.1 us per pass at 65 536 envs, not kept)
+  // (float pairs per store: 128 vs 137.7 us per step at 65 536 envs in the pipelined kernel, profiles/r06/s27;
+  // in the first row-per-wave kernel they had been slower, 94.7 vs 81.1 us per pass)
   const bool one = a.D <= kFlatU * 64 && a.OB <= 2048;  // (rows of one pass; the bytes fit the LDS window)
-  const void* fn = h->flat_dtype ? (one ? (const void*)k_flatten<int8_t, true> : (const void*)k_flatten<int8_t, false>)
-                                 : (one ? (const void*)k_flatten<float, true> : (const void*)k_flatten<float, false>);
+  const bool pair = one && !h->flat_dtype && a.D % 2 == 0;  // float pairs: rows 8-byte aligned, none straddles D
+  const void* fn = h->flat_dtype ? (one ? (const void*)k_flatten<int8_t, true, 1> : (const void*)k_flatten<int8_t, false, 1>)
+                                 : (pair ? (const void*)k_flatten<float, true, 2>
+                                         : (one ? (const void*)k_flatten<float, true, 1> : (const void*)k_flatten<float, false, 1>));
   if (h->flat_fn != fn) {  // the workgroups resident at once (kernel registers), fixed per variant
     int ncu = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || ncu < 1) ncu = 256;
@@ -5322,11 +5352,13 @@ static int launch_flatten(pgtg_handle* h, int mode) {
   // envs, profiles/r06/flat_grid_sweep.txt -- the kernel is bound chip-wide, not by waves in flight)
   const uint64_t G = std::max<uint64_t>(std::min<uint64_t>(h->n, h->flat_wgs), (h->n + 255) / 256);
   if (h->flat_dtype) {
-    if (one) hipLaunchKernelGGL((k_flatten<int8_t, true>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
-    else hipLaunchKernelGGL((k_flatten<int8_t, false>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
+    if (one) hipLaunchKernelGGL((k_flatten<int8_t, true, 1>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
+    else hipLaunchKernelGGL((k_flatten<int8_t, false, 1>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
+  } else if (pair) {
+    hipLaunchKernelGGL((k_flatten<float, true, 2>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
   } else {
-    if (one) hipLaunchKernelGGL((k_flatten<float, true>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
-    else hipLaunchKernelGGL((k_flatten<float, false>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
+    if (one) hipLaunchKernelGGL((k_flatten<float, true, 1>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
+    else hipLaunchKernelGGL((k_flatten<float, false, 1>), dim3((unsigned)G), dim3(256), 0, h->stream, a);
   }
   HIPCHK(h, hipGetLastError());
   return PGTG_OK;
